@@ -1,0 +1,1625 @@
+// hftlob.hip — MI355X (gfx950 / CDNA4) limit-order-book engine and fused
+// multi-agent env step, behind the C ABI of include/hftlob.h.
+//
+// Execution model: ONE 64-lane wavefront per environment.  An order-book side
+// of nO slots lives in VGPRs lane-strided (slot s -> lane s&63, register set
+// s>>6, S = ceil(nO/64) sets), the trade log likewise, and the message stream
+// is held 64 rows at a time (row m -> lane m&63).  Each message is decoded into
+// SGPRs with v_readlane, so the per-message type dispatch is a wave-uniform
+// scalar branch (only the taken handler runs — the XLA reference evaluates all
+// five lax.switch branches under vmap).  Price-time priority, first-free-slot,
+// best-quote and volume queries are DPP wave reductions and ballots.  Single
+// slots are updated with v_writelane.  No LDS for book state; a 4 KB LDS
+// staging area holds the agents' message rows of the fused step.
+//
+// Semantics follow the reference line by line (cited per function), including
+// its quirks.  Integer state is bit-exact with the
+// oracle; float32 arithmetic follows the jnp expression order, and float sums
+// use the canonical wave order (fold lane l+64k, then xor butterfly 32..1).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <limits.h>
+
+#include "../../include/hftlob.h"
+
+typedef int32_t i32;
+typedef uint32_t u32;
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- wave utils
+DEV int lane_id() { return __lane_id(); }
+DEV i32 rdl(i32 v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEV i32 wrl(i32 old, i32 val, int l) { return __lane_id() == l ? val : old; }  // v_cmp + v_cndmask
+DEV i32 uni(i32 v) { return __builtin_amdgcn_readfirstlane(v); }
+DEV float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+DEV i32 wadd(i32 a, i32 b) { return (i32)((u32)a + (u32)b); }
+DEV i32 wsub(i32 a, i32 b) { return (i32)((u32)a - (u32)b); }
+DEV i32 wmul(i32 a, i32 b) { return (i32)((u32)a * (u32)b); }
+DEV i32 iabs_(i32 a) { return a < 0 ? wsub(0, a) : a; }
+DEV i32 isign(i32 a) { return (a > 0) - (a < 0); }
+DEV i32 imax_(i32 a, i32 b) { return a > b ? a : b; }
+DEV i32 imin_(i32 a, i32 b) { return a < b ? a : b; }
+DEV float i2f(i32 a) { return (float)a; }
+DEV i32 f2i(float f) { return (i32)f; }
+DEV float bitf(i32 w) { return __int_as_float(w); }
+DEV i32 fbit(float f) { return __float_as_int(f); }
+
+// jnp.floor_divide for int32
+DEV i32 ifloordiv(i32 a, i32 b) {
+    i32 q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
+    return q;
+}
+// jnp.floor_divide for float32 (jax _float_divmod, round half away from zero)
+DEV float ffloordiv(float x, float y) {
+    float mod = fmodf(x, y);
+    float div = (x - mod) / y;
+    bool ind = (mod != 0.0f) && (((y > 0) - (y < 0)) != ((mod > 0) - (mod < 0)));
+    if (ind) div = div - 1.0f;
+    return roundf(div);
+}
+
+// DPP all-reduce across the wave; result is wave-uniform (SGPR).
+// quad_perm[1,0,3,2], quad_perm[2,3,0,1], row_half_mirror, row_mirror,
+// row_bcast:15 (rows 1,3), row_bcast:31 (rows 2,3) -> lane 63 holds the total.
+#define DPPX(idv, v, ctrl, rmask) __builtin_amdgcn_update_dpp((idv), (v), (ctrl), (rmask), 0xF, false)
+DEV i32 wave_max(i32 v) {
+    v = imax_(v, DPPX(INT_MIN, v, 0xB1, 0xF));
+    v = imax_(v, DPPX(INT_MIN, v, 0x4E, 0xF));
+    v = imax_(v, DPPX(INT_MIN, v, 0x141, 0xF));
+    v = imax_(v, DPPX(INT_MIN, v, 0x140, 0xF));
+    v = imax_(v, DPPX(INT_MIN, v, 0x142, 0xA));
+    v = imax_(v, DPPX(INT_MIN, v, 0x143, 0xC));
+    return rdl(v, 63);
+}
+DEV i32 wave_min(i32 v) {
+    v = imin_(v, DPPX(INT_MAX, v, 0xB1, 0xF));
+    v = imin_(v, DPPX(INT_MAX, v, 0x4E, 0xF));
+    v = imin_(v, DPPX(INT_MAX, v, 0x141, 0xF));
+    v = imin_(v, DPPX(INT_MAX, v, 0x140, 0xF));
+    v = imin_(v, DPPX(INT_MAX, v, 0x142, 0xA));
+    v = imin_(v, DPPX(INT_MAX, v, 0x143, 0xC));
+    return rdl(v, 63);
+}
+DEV i32 wave_sum(i32 v) {
+    v = wadd(v, DPPX(0, v, 0xB1, 0xF));
+    v = wadd(v, DPPX(0, v, 0x4E, 0xF));
+    v = wadd(v, DPPX(0, v, 0x141, 0xF));
+    v = wadd(v, DPPX(0, v, 0x140, 0xF));
+    v = wadd(v, DPPX(0, v, 0x142, 0xA));
+    v = wadd(v, DPPX(0, v, 0x143, 0xC));
+    return rdl(v, 63);
+}
+// canonical float sum (order fixed; the C oracle emulates it bit for bit)
+DEV float wave_fsum(float v) {
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) v = v + __shfl_xor(v, k, 64);
+    return unif(v);
+}
+DEV unsigned long long ballot(bool p) { return __ballot(p); }
+
+// ------------------------------------------------------------------ PRNG
+DEV u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
+DEV void threefry(u32 k0, u32 k1, u32 x0, u32 x1, u32& o0, u32& o1) {
+    const u32 k2 = k0 ^ k1 ^ 0x1BD11BDAu;
+    x0 += k0;
+    x1 += k1;
+#define TF_R(r) x0 += x1; x1 = rotl32(x1, r); x1 ^= x0;
+#define TF_G1 TF_R(13) TF_R(15) TF_R(26) TF_R(6)
+#define TF_G2 TF_R(17) TF_R(29) TF_R(16) TF_R(24)
+    TF_G1 x0 += k1; x1 += k2 + 1u;
+    TF_G2 x0 += k2; x1 += k0 + 2u;
+    TF_G1 x0 += k0; x1 += k1 + 3u;
+    TF_G2 x0 += k1; x1 += k2 + 4u;
+    TF_G1 x0 += k2; x1 += k0 + 5u;
+#undef TF_G1
+#undef TF_G2
+#undef TF_R
+    o0 = x0;
+    o1 = x1;
+}
+struct Key { u32 a, b; };
+// jax.random.split(key, n)[j]
+DEV Key split_key(Key k, int n, int j, bool part) {
+    Key o;
+    if (part) { threefry(k.a, k.b, 0u, (u32)j, o.a, o.b); return o; }
+    u32 y0, y1;
+    int m = 2 * j;
+    if (m < n) { threefry(k.a, k.b, (u32)m, (u32)(n + m), y0, y1); o.a = y0; }
+    else { threefry(k.a, k.b, (u32)(m - n), (u32)m, y0, y1); o.a = y1; }
+    m = 2 * j + 1;
+    if (m < n) { threefry(k.a, k.b, (u32)m, (u32)(n + m), y0, y1); o.b = y0; }
+    else { threefry(k.a, k.b, (u32)(m - n), (u32)m, y0, y1); o.b = y1; }
+    return o;
+}
+// jax random_bits(key, 32, (n,))[i]
+DEV u32 random_bits(Key k, int n, int i, bool part) {
+    u32 y0, y1;
+    if (part) { threefry(k.a, k.b, 0u, (u32)i, y0, y1); return y0 ^ y1; }
+    int half = (n + 1) / 2;
+    if (i < half) {
+        threefry(k.a, k.b, (u32)i, (i + half < n) ? (u32)(i + half) : 0u, y0, y1);
+        return y0;
+    }
+    threefry(k.a, k.b, (u32)(i - half), (i < n) ? (u32)i : 0u, y0, y1);
+    return y1;
+}
+// jax.random.randint(key, (), lo, hi), int32
+DEV i32 randint(Key k, i32 lo, i32 hi, bool part) {
+    Key k1 = split_key(k, 2, 0, part), k2 = split_key(k, 2, 1, part);
+    u32 hb = random_bits(k1, 1, 0, part), lb = random_bits(k2, 1, 0, part);
+    u32 span = (hi <= lo) ? 1u : (u32)hi - (u32)lo;
+    u32 mult = 65536u % span;
+    mult = (mult * mult) % span;
+    u32 off = ((hb % span) * mult + (lb % span)) % span;
+    return (i32)((u32)lo + off);
+}
+
+// --------------------------------------------------------- book side state
+struct LobCfg {
+    i32 maxint, init_id, depth, cancel_mode, t4, check_fill, nO, nT;
+};
+DEV LobCfg lobcfg(const hftlob_lob_cfg& c) {
+    LobCfg o;
+    o.maxint = c.maxint; o.init_id = c.init_id; o.depth = c.book_depth; o.cancel_mode = c.cancel_mode;
+    o.t4 = c.type_4_interpretation; o.check_fill = c.check_book_fill; o.nO = c.n_orders; o.nT = c.n_trades;
+    return o;
+}
+
+template <int S>
+struct Side {
+    i32 p[S], q[S], oid[S], tid[S], ts[S], tns[S];
+    i32 best_p, best_q;  // cached (price, volume) of get_best_*; valid when ok
+    bool ok;             // cache valid
+    bool clean;          // every slot with q <= 0 is an all -1 row (see rzn)
+};
+
+// uniform-index slot access
+template <int S> DEV i32 sget(const i32 (&a)[S], int idx) {
+    const int r = idx >> 6, l = idx & 63;
+    i32 v = rdl(a[0], l);
+#pragma unroll
+    for (int k = 1; k < S; ++k) if (r == k) v = rdl(a[k], l);
+    return v;
+}
+template <int S> DEV void sset(i32 (&a)[S], int idx, i32 val) {
+    const int r = idx >> 6, l = idx & 63;
+#pragma unroll
+    for (int k = 0; k < S; ++k) if (r == k) a[k] = wrl(a[k], val, l);
+}
+template <int S> DEV void clear_slot(Side<S>& s, int idx) {
+    sset(s.p, idx, -1); sset(s.q, idx, -1); sset(s.oid, idx, -1);
+    sset(s.tid, idx, -1); sset(s.ts, idx, -1); sset(s.tns, idx, -1);
+}
+template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        unsigned long long b = ballot(pr[r]);
+        if (b) return r * 64 + (int)__builtin_ctzll(b);
+    }
+    return fallback;
+}
+
+template <int S>
+struct Valid {
+    bool v[S];
+    DEV void init(int n) {
+        const int l = lane_id();
+#pragma unroll
+        for (int r = 0; r < S; ++r) v[r] = r * 64 + l < n;
+    }
+};
+
+template <int S> DEV void load_side(Side<S>& s, const i32* g, const Valid<S>& V) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const int sl = r * 64 + l;
+        if (V.v[r]) {
+            const int2* row = reinterpret_cast<const int2*>(g + sl * 6);
+            int2 x0 = row[0], x1 = row[1], x2 = row[2];
+            s.p[r] = x0.x; s.q[r] = x0.y; s.oid[r] = x1.x; s.tid[r] = x1.y; s.ts[r] = x2.x; s.tns[r] = x2.y;
+        } else {
+            s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
+        }
+    }
+    // clean: every slot with q <= 0 is all -1 (then targeted removal == _removeZeroNegQuant)
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < S; ++r)
+        bad |= V.v[r] && s.q[r] <= 0 &&
+               !(s.p[r] == -1 && s.q[r] == -1 && s.oid[r] == -1 && s.tid[r] == -1 && s.ts[r] == -1 && s.tns[r] == -1);
+    s.clean = ballot(bad) == 0ull;
+    s.ok = false;
+}
+template <int S> DEV void store_side(const Side<S>& s, i32* g, const Valid<S>& V) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        if (V.v[r]) {
+            int2* row = reinterpret_cast<int2*>(g + (r * 64 + l) * 6);
+            row[0] = make_int2(s.p[r], s.q[r]);
+            row[1] = make_int2(s.oid[r], s.tid[r]);
+            row[2] = make_int2(s.ts[r], s.tns[r]);
+        }
+    }
+}
+
+// _removeZeroNegQuant — JaxOrderBookArrays.py:85-90.  Full pass over the side
+// when the side may hold stray q<=0 rows, else only the slot just written.
+template <int S> DEV void rzn(Side<S>& s, int idx, const Valid<S>& V) {
+    if (s.clean) {
+        if (sget(s.q, idx) <= 0) clear_slot(s, idx);
+    } else {
+#pragma unroll
+        for (int r = 0; r < S; ++r)
+            if (s.q[r] <= 0) s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
+        s.clean = true;
+        s.ok = false;
+    }
+}
+
+// get_best_bid: max raw price (empty side -> -1); volume at it — :943-951,906-917
+template <int S> DEV void best_bid(Side<S>& s, const Valid<S>& V) {
+    i32 m = INT_MIN;
+#pragma unroll
+    for (int r = 0; r < S; ++r) m = imax_(m, V.v[r] ? s.p[r] : INT_MIN);
+    const i32 mp = wave_max(m);
+    i32 v = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.p[r] == mp) ? s.q[r] : 0);
+    s.best_p = mp;
+    s.best_q = wave_sum(v);
+    s.ok = true;
+}
+// get_best_ask: min price with -1 -> maxint, maxint -> -1; volume at it — :932-941
+template <int S> DEV void best_ask(Side<S>& s, const Valid<S>& V, i32 maxint) {
+    i32 m = INT_MAX;
+#pragma unroll
+    for (int r = 0; r < S; ++r) m = imin_(m, V.v[r] ? (s.p[r] == -1 ? maxint : s.p[r]) : INT_MAX);
+    i32 mn = wave_min(m);
+    const i32 pa = mn == maxint ? -1 : mn;
+    i32 v = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.p[r] == pa) ? s.q[r] : 0);
+    s.best_p = pa;
+    s.best_q = wave_sum(v);
+    s.ok = true;
+}
+
+// _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas)
+template <bool BID, int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, const LobCfg& c, i32 mp) {
+    i32 t[S], n[S], m = INT_MAX;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        t[r] = (s.p[r] == mp) ? s.ts[r] : c.maxint;
+        m = imin_(m, V.v[r] ? t[r] : INT_MAX);
+    }
+    const i32 mts = wave_min(m);
+    m = INT_MAX;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        n[r] = (t[r] == mts) ? s.tns[r] : c.maxint;
+        m = imin_(m, V.v[r] ? n[r] : INT_MAX);
+    }
+    const i32 mtn = wave_min(m);
+    bool pr[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) pr[r] = V.v[r] && n[r] == mtn;
+    return first_true(pr, c.nO - 1);
+}
+
+// ------------------------------------------------------------ trade log
+template <int S>
+struct Trades {
+    i32 f[8][S];
+};
+template <int S> DEV void trades_fill(Trades<S>& T, i32 v) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int r = 0; r < S; ++r) T.f[k][r] = v;
+}
+template <int S> DEV void load_trades(Trades<S>& T, const i32* g, const Valid<S>& V) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        if (V.v[r]) {
+            const int4* row = reinterpret_cast<const int4*>(g + (r * 64 + l) * 8);
+            int4 a = row[0], b = row[1];
+            T.f[0][r] = a.x; T.f[1][r] = a.y; T.f[2][r] = a.z; T.f[3][r] = a.w;
+            T.f[4][r] = b.x; T.f[5][r] = b.y; T.f[6][r] = b.z; T.f[7][r] = b.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) T.f[k][r] = -1;
+        }
+    }
+}
+template <int S> DEV void store_trades(const Trades<S>& T, i32* g, const Valid<S>& V) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        if (V.v[r]) {
+            int4* row = reinterpret_cast<int4*>(g + (r * 64 + l) * 8);
+            row[0] = make_int4(T.f[0][r], T.f[1][r], T.f[2][r], T.f[3][r]);
+            row[1] = make_int4(T.f[4][r], T.f[5][r], T.f[6][r], T.f[7][r]);
+        }
+    }
+}
+
+// ------------------------------------------------------ message handlers
+template <int S>
+struct Book {
+    Side<S> a, b;
+    Trades<S> tr;
+    Valid<S> vs, vt;
+    LobCfg c;
+};
+
+struct Msg {
+    i32 type, side, price, qty, oid, tid, t, tns;
+};
+
+// match_order — JaxOrderBookArrays.py:172-220
+template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
+    const i32 qt = sget(s.q, top), pt = sget(s.p, top), ot = sget(s.oid, top), tt = sget(s.tid, top);
+    const i32 newq = imax_(0, wsub(qt, qtm));
+    const i32 rem = wsub(qtm, qt);
+    bool pr[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) pr[r] = B.vt.v[r] && B.tr.f[4][r] == -1;  // trade[:,OID=4] == -1
+    const int e = first_true(pr, B.c.nT - 1);
+    sset(B.tr.f[0], e, pt);
+    sset(B.tr.f[1], e, wmul(wsub(0, m.side), wsub(qt, newq)));
+    sset(B.tr.f[2], e, ot);
+    sset(B.tr.f[3], e, m.oid);
+    sset(B.tr.f[4], e, m.t);
+    sset(B.tr.f[5], e, m.tns);
+    sset(B.tr.f[6], e, tt);
+    sset(B.tr.f[7], e, m.tid);
+    sset(s.q, top, newq);
+    rzn(s, top, B.vs);
+    s.ok = false;
+    return rem;
+}
+
+// _match_against_{bid,ask}_orders — :284-331.  `mp` shortcut: the top slot's
+// price never beats the side's best, so "best does not cross" ends the loop
+// exactly; only a crossing best pays for the full 3-reduction top-of-book.
+template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
+    while (qtm > 0) {
+        if (!s.ok) { if (BID) best_bid(s, B.vs); else best_ask(s, B.vs, B.c.maxint); }
+        const i32 mp = BID ? s.best_p : (s.best_p == -1 ? B.c.maxint : s.best_p);
+        if (BID ? !(mp >= price) : !(mp <= price)) break;
+        const int top = top_idx<BID>(s, B.vs, B.c, mp);
+        const i32 tp = sget(s.p, top);
+        if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
+        qtm = match_order(B, s, top, qtm, m);
+    }
+    return qtm;
+}
+
+// add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
+template <int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
+    bool pr[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r)
+        pr[r] = B.vs.v[r] && (s.p[r] == -1 || s.q[r] == -1 || s.oid[r] == -1 || s.tid[r] == -1 ||
+                              s.ts[r] == -1 || s.tns[r] == -1);
+    const int e = first_true(pr, B.c.nO - 1);
+    sset(s.p, e, m.price); sset(s.q, e, imax_(0, qty)); sset(s.oid, e, m.oid);
+    sset(s.tid, e, m.tid); sset(s.ts, e, m.t);          sset(s.tns, e, m.tns);
+    rzn(s, e, B.vs);
+    s.ok = false;
+}
+
+// check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max)
+template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
+    bool neg = false;
+    i32 w = BID ? INT_MAX : INT_MIN;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        neg |= B.vs.v[r] && s.p[r] < 0;
+        w = BID ? imin_(w, B.vs.v[r] ? s.p[r] : INT_MAX) : imax_(w, B.vs.v[r] ? s.p[r] : INT_MIN);
+    }
+    if (ballot(neg) != 0ull) return;
+    const i32 worst = BID ? wave_min(w) : wave_max(w);
+#pragma unroll
+    for (int r = 0; r < S; ++r)
+        if (s.p[r] == worst) s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
+    s.ok = false;
+}
+
+// bid_lim — :357-420
+template <int S> DEV void bid_lim(Book<S>& B, Msg m) {
+    const i32 rem = match_against<false>(B, B.a, m.qty, m.price, m);
+    if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
+    if (B.c.check_fill) evict_if_full<true>(B, B.b);
+    const bool discard = (B.c.t4 == 0 || B.c.t4 == 2) && m.type == 4;
+    if (!discard) add_order(B, B.b, m, rem);
+}
+// ask_lim — :446-508
+template <int S> DEV void ask_lim(Book<S>& B, Msg m) {
+    if (B.c.t4 == 2) m.price = 0;
+    const i32 rem = match_against<true>(B, B.b, m.qty, m.price, m);
+    if (B.c.check_fill) evict_if_full<false>(B, B.a);
+    const bool discard = (B.c.t4 == 0 || B.c.t4 == 2) && m.type == 4;
+    if (!discard) add_order(B, B.a, m, rem);
+}
+// cancel_order + get_init_id_match — :93-139
+template <int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+    bool pr[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) pr[r] = B.vs.v[r] && s.oid[r] == m.oid;
+    int idx = first_true(pr, -1);
+    if (idx < 0) {
+        const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
+#pragma unroll
+        for (int r = 0; r < S; ++r)
+            pr[r] = B.vs.v[r] && s.p[r] == m.price && s.oid[r] <= B.c.init_id && s.oid[r] >= lo && s.q[r] >= m.qty;
+        idx = first_true(pr, B.c.nO - 1);  // -1 wraps to the last slot
+    }
+    const i32 old_p = sget(s.p, idx);
+    sset(s.q, idx, wsub(sget(s.q, idx), m.qty));
+    const bool was_clean = s.clean;
+    rzn(s, idx, B.vs);
+    // best quote unchanged iff the touched slot was neither at the best price
+    // nor empty and the side was not empty (price/volume sets then unchanged)
+    if (!(was_clean && s.ok && old_p != s.best_p && old_p != -1 && s.best_p != -1)) s.ok = false;
+}
+
+// cond_type_side_save_bidask — :687-732 (dispatch index exactly as reference)
+template <int S> DEV void process_msg(Book<S>& B, i32 d0, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+    Msg m;
+    m.type = d0;
+    m.side = d0 == 4 ? wsub(0, d1) : d1;
+    m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
+    const bool lim = (m.type == 1) || (m.type == 4), cnl = (m.type == 2) || (m.type == 3);
+    const int index = (m.side == 1 && lim) * 1 + (m.side == -1 && cnl) * 2 + (m.side == 1 && cnl) * 3 +
+                      (m.side == 0 && m.type == 0) * 4;
+    if (index == 0) ask_lim(B, m);
+    else if (index == 1) bid_lim(B, m);
+    else if (index == 2) cancel(B, B.a, m);
+    else if (index == 3) cancel(B, B.b, m);
+}
+template <int S> DEV void refresh_best(Book<S>& B) {
+    if (!B.a.ok) best_ask(B.a, B.vs, B.c.maxint);
+    if (!B.b.ok) best_bid(B.b, B.vs);
+}
+
+// ================================================= K1: book_process kernel
+// scan_through_entire_array[_save_bidask] — JaxOrderBookArrays.py:736-823
+template <int S>
+__global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
+                                                     i32* __restrict__ asks, i32* __restrict__ bids,
+                                                     i32* __restrict__ trades, i32* __restrict__ best_asks,
+                                                     i32* __restrict__ best_bids) {
+    const int e = blockIdx.x;
+    if (e >= n_env) return;
+    const int l = lane_id();
+    Book<S> B;
+    B.c = lobcfg(cfg);
+    B.vs.init(B.c.nO);
+    B.vt.init(B.c.nT);
+    i32* ga = asks + (size_t)e * B.c.nO * 6;
+    i32* gb = bids + (size_t)e * B.c.nO * 6;
+    i32* gt = trades + (size_t)e * B.c.nT * 8;
+    load_side(B.a, ga, B.vs);
+    load_side(B.b, gb, B.vs);
+    load_trades(B.tr, gt, B.vt);
+    const i32* gm = msgs + (size_t)e * n_msg * 8;
+    for (int base = 0; base < n_msg; base += 64) {
+        const int row = base + l;
+        int4 x = make_int4(0, 0, 0, 0), y = x;
+        if (row < n_msg) {
+            x = reinterpret_cast<const int4*>(gm + row * 8)[0];
+            y = reinterpret_cast<const int4*>(gm + row * 8)[1];
+        }
+        i32 ap = 0, aq = 0, bp = 0, bq = 0;
+        const int cnt = imin_(64, n_msg - base);
+        for (int k = 0; k < cnt; ++k) {
+            process_msg(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
+                        rdl(y.z, k), rdl(y.w, k));
+            if (best_asks) {
+                refresh_best(B);
+                ap = wrl(ap, B.a.best_p, k); aq = wrl(aq, B.a.best_q, k);
+                bp = wrl(bp, B.b.best_p, k); bq = wrl(bq, B.b.best_q, k);
+            }
+        }
+        if (best_asks && row < n_msg) {
+            reinterpret_cast<int2*>(best_asks + ((size_t)e * n_msg + row) * 2)[0] = make_int2(ap, aq);
+            reinterpret_cast<int2*>(best_bids + ((size_t)e * n_msg + row) * 2)[0] = make_int2(bp, bq);
+        }
+    }
+    store_side(B.a, ga, B.vs);
+    store_side(B.b, gb, B.vs);
+    store_trades(B.tr, gt, B.vt);
+}
+
+// =========================================================== env helpers
+struct EnvCfg {
+    const hftlob_env_cfg* c;
+};
+
+// world/loaded word indices inside the record (hftlob.h)
+enum { LD_T0 = 0, LD_T1, LD_WIN, LD_MAXS, LD_START, LD_STEP };
+enum { W_T0 = 0, W_T1, W_OIDC, W_MID, W_DT };
+
+DEV int agent_words(const hftlob_agent_type_cfg& t) { return t.kind == HFTLOB_AGENT_MM ? 5 : 13; }
+
+// side volume (get_volume — :919-930)
+template <int S> DEV i32 side_volume(const Side<S>& s, const Valid<S>& V) {
+    i32 v = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.p[r] != -1) ? s.q[r] : 0);
+    return wave_sum(v);
+}
+
+// canonical float sum of per-row values over n rows held S-strided
+template <int S> DEV float rows_fsum(const float (&x)[S], int n) {
+    const int l = lane_id();
+    float a = l < n ? x[0] : 0.0f;
+#pragma unroll
+    for (int r = 1; r < S; ++r) if (r * 64 + l < n) a = a + x[r];
+    return wave_fsum(a);
+}
+
+struct Obs {
+    float v[HFTLOB_MAX_OBS];
+};
+
+struct WorldView {  // wave-uniform world quantities used by obs
+    i32 best_ask_p, best_bid_p, vol_a, vol_b, step, max_steps;
+    float mid;
+};
+
+// MM _get_obs_basic / _get_obs_engineered (fixed_steps), sorted keys — mm_env.py:2963-3154
+DEV void mm_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o) {
+    const bool nz = tc.normalize;
+    const i32 spread = iabs_(wsub(w.best_ask_p, w.best_bid_p));
+    if (tc.observation_space == HFTLOB_MM_OBS_BASIC) {
+        o[0] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
+        o[1] = nz ? i2f(spread) / 1e4f : i2f(spread);
+        return;
+    }
+    o[0] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
+    o[1] = nz ? w.mid / 1e6f : w.mid;
+    o[2] = nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p);
+    o[3] = nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p);
+    o[4] = nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a);
+    o[5] = nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b);
+    o[6] = nz ? i2f(spread) / 1e4f : i2f(spread);
+    o[7] = nz ? i2f(w.step) / 10.0f : i2f(w.step);
+}
+// EXE _get_obs (fixed_steps), sorted keys — exec_env.py:1913-2079
+DEV void exe_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o) {
+    const bool nz = tc.normalize;
+    const i32 sell = st[3];
+    const i32 p_aggr = sell ? w.best_bid_p : w.best_ask_p, p_pass = sell ? w.best_ask_p : w.best_bid_p;
+    const i32 q_aggr = sell ? w.vol_b : w.vol_a, q_pass = sell ? w.vol_a : w.vol_b;
+    const float ip = bitf(st[0]);
+    const float ts = (float)tc.task_size;
+    const float rr = w.max_steps == 0 ? 0.0f : 1.0f - i2f(w.step) / i2f(w.max_steps);
+    if (nz) {
+        o[0] = i2f(st[2]) / ts;
+        o[1] = ip / 1e7f;
+        o[2] = i2f(sell) / 1.0f;
+        o[3] = (i2f(p_aggr) - ip) / 1e5f;
+        o[4] = (i2f(p_pass) - ip) / 1e5f;
+        o[5] = i2f(q_aggr) / 1000.0f;
+        o[6] = i2f(q_pass) / 1000.0f;
+        o[7] = i2f(wsub(st[1], st[2])) / ts;
+        o[8] = rr / 1.0f;
+        o[9] = i2f(iabs_(wsub(p_aggr, p_pass))) / 1e4f;
+        o[10] = i2f(w.step) / 30.0f;
+        o[11] = i2f(st[1]) / ts;
+    } else {
+        o[0] = i2f(st[2]); o[1] = ip; o[2] = i2f(sell); o[3] = i2f(p_aggr); o[4] = i2f(p_pass);
+        o[5] = i2f(q_aggr); o[6] = i2f(q_pass); o[7] = i2f(wsub(st[1], st[2])); o[8] = rr;
+        o[9] = i2f(iabs_(wsub(p_aggr, p_pass))); o[10] = i2f(w.step); o[11] = i2f(st[1]);
+    }
+}
+// write one agent's obs row (lanes 0..obs_stride-1 store one float each)
+DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st,
+                   float* dst, bool zero) {
+    float o[HFTLOB_MAX_OBS];
+#pragma unroll
+    for (int k = 0; k < HFTLOB_MAX_OBS; ++k) o[k] = 0.0f;
+    if (tc.kind == HFTLOB_AGENT_MM) mm_obs(tc, w, st, o);
+    else exe_obs(tc, w, st, o);
+    const int l = lane_id();
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < HFTLOB_MAX_OBS; ++k) if (l == k) v = o[k];
+    if (zero) v = 0.0f;
+    if (l < c.obs_stride) dst[l] = v;
+}
+
+// ----------------------------------------- reset (MARLEnv.reset_env) device
+// marl_env.py:129-207; BaseLOBEnv.reset_env base_env.py:218-234; agents
+// mm_env.py:417-459, exec_env.py:209-266.  Writes the whole record + obs.
+template <int S>
+DEV void env_reset_dev(const hftlob_env_cfg& c, Key key, const i32* __restrict__ init_states, i32* __restrict__ rec,
+                       float* __restrict__ obs, const Valid<S>& VS, const Valid<S>& VT) {
+    const bool part = c.prng_partitionable;
+    const int nTy = c.n_types, l = lane_id();
+    Key wk = split_key(key, nTy + 1, nTy, part);
+    i32 idx = c.window_selector == -1 ? randint(wk, 0, c.n_windows, part) : c.window_selector;
+    idx = imin_(imax_(idx, 0), c.n_windows - 1);
+    const i32* src = init_states + (size_t)idx * c.init_rec_words;
+    // copy the LoadedEnvState prefix (asks, bids, trades, 6 scalars), 16B vectors
+    for (int w = l * 4; w < c.init_rec_words; w += 256) {
+        if (w + 3 < c.init_rec_words) {
+            *reinterpret_cast<int4*>(rec + w) = *reinterpret_cast<const int4*>(src + w);
+        } else {
+            for (int k = w; k < c.init_rec_words; ++k) rec[k] = src[k];
+        }
+    }
+    Side<S> a, b;
+    load_side(a, src + c.off_asks, VS);
+    load_side(b, src + c.off_bids, VS);
+    best_ask(a, VS, c.lob.maxint);
+    best_bid(b, VS);
+    // tile best quotes over M rows
+    for (int m = l; m < c.n_msgs; m += 64) {
+        reinterpret_cast<int2*>(rec + c.off_best_asks)[m] = make_int2(a.best_p, a.best_q);
+        reinterpret_cast<int2*>(rec + c.off_best_bids)[m] = make_int2(b.best_p, b.best_q);
+    }
+    const float mid = i2f(wadd(b.best_p, a.best_p)) / 2.0f;
+    const i32 t0 = src[c.off_loaded + LD_T0], t1 = src[c.off_loaded + LD_T1];
+    if (l == 0) {
+        i32* W = rec + c.off_world;
+        W[W_T0] = t0; W[W_T1] = t1; W[W_OIDC] = c.order_id_counter_start; W[W_MID] = fbit(mid); W[W_DT] = fbit(0.0f);
+    }
+    WorldView wv;
+    wv.best_ask_p = a.best_p; wv.best_bid_p = b.best_p;
+    wv.vol_a = side_volume(a, VS); wv.vol_b = side_volume(b, VS);
+    wv.step = src[c.off_loaded + LD_STEP]; wv.max_steps = src[c.off_loaded + LD_MAXS]; wv.mid = mid;
+    // zero the record's padding words (after the world block, after the agents)
+    int agents_end = c.off_agents;
+    for (int t = 0; t < nTy; ++t) agents_end += c.types[t].n_agents * agent_words(c.types[t]);
+    for (int w = c.off_world + 5 + l; w < c.off_agents; w += 64) rec[w] = 0;
+    for (int w = agents_end + l; w < c.rec_words; w += 64) rec[w] = 0;
+    i32* st = rec + c.off_agents;
+    int ag = 0;
+    for (int t = 0; t < nTy; ++t) {
+        const hftlob_agent_type_cfg& tc = c.types[t];
+        i32 sell = tc.task == HFTLOB_TASK_SELL ? 1 : 0;
+        if (tc.kind == HFTLOB_AGENT_EXE && tc.task == HFTLOB_TASK_RANDOM)
+            sell = randint(split_key(key, nTy + 1, t, part), 0, 2, part);
+        for (int i = 0; i < tc.n_agents; ++i, ++ag) {
+            i32 s[13];
+            if (tc.kind == HFTLOB_AGENT_MM) {
+                s[0] = 0; s[1] = 0; s[2] = 0; s[3] = fbit(0.0f); s[4] = fbit(0.0f);
+            } else {
+                s[0] = fbit(mid); s[1] = tc.task_size; s[2] = 0; s[3] = sell; s[4] = fbit(mid / (float)c.tick_size);
+                for (int k = 5; k < 13; ++k) s[k] = fbit(0.0f);
+            }
+            const int nw = agent_words(tc);
+            i32 v = 0;
+            for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
+            if (l < nw) st[l] = v;
+            if (obs) write_obs(c, tc, wv, s, obs + (size_t)ag * c.obs_stride, false);
+            st += nw;
+        }
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(64) void k_env_reset(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
+                                                  const i32* __restrict__ init_states, i32* __restrict__ state,
+                                                  float* __restrict__ obs) {
+    const int e = blockIdx.x;
+    if (e >= n_env) return;
+    Valid<S> VS, VT;
+    VS.init(c.lob.n_orders);
+    VT.init(c.lob.n_trades);
+    Key k{keys[2 * e], keys[2 * e + 1]};
+    env_reset_dev<S>(c, k, init_states, state + (size_t)e * c.rec_words,
+                     obs ? obs + (size_t)e * c.n_agents * c.obs_stride : nullptr, VS, VT);
+}
+
+// ------------------------------------------------------------ agent logic
+struct ActX {
+    i32 bid_price, ask_price, bid_dist, ask_dist, bid_quant, ask_quant;
+};
+
+// write one 8-int message row into the LDS staging area (lane 0..7 each write a field)
+DEV void put_row(i32* lds_rows, int row, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5, i32 f6, i32 f7) {
+    const int l = lane_id();
+    i32 v = f0;
+    v = l == 1 ? f1 : v; v = l == 2 ? f2 : v; v = l == 3 ? f3 : v;
+    v = l == 4 ? f4 : v; v = l == 5 ? f5 : v; v = l == 6 ? f6 : v; v = l == 7 ? f7 : v;
+    if (l < 8) lds_rows[row * 8 + l] = v;
+}
+DEV i32 get_field(const i32* lds_rows, int row, int f) { return uni(lds_rows[row * 8 + f]); }
+
+// getCancelMsgs — JaxOrderBookArrays.py:827-853
+template <int S>
+DEV void cancel_rows(const Side<S>& s, const Valid<S>& V, i32 agent, int size, i32 side, i32 t, i32 tns,
+                     i32* lds_rows, int row0) {
+    int n = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        unsigned long long bm = ballot(V.v[r] && s.tid[r] == agent);
+        while (bm && n < size) {
+            const int l = (int)__builtin_ctzll(bm);
+            bm &= bm - 1;
+            put_row(lds_rows, row0 + n, 2, side, rdl(s.q[r], l), rdl(s.p[r], l), rdl(s.oid[r], l),
+                    rdl(s.tid[r], l), t, tns);
+            ++n;
+        }
+    }
+    for (; n < size; ++n) put_row(lds_rows, row0 + n, 2, side, 0, 0, 0, 0, t, tns);
+}
+
+// _filter_messages — mm_env.py:520-582 == exec_env.py:413-475 (N rows, scalar)
+template <int n>
+DEV void filter_rows(i32* lds_rows, int arow, int crow) {
+    __syncthreads();
+    i32 ap[n], aqv[n], cp[n], cq[n];
+    for (int i = 0; i < n; ++i) {
+        ap[i] = get_field(lds_rows, arow + i, 3); aqv[i] = get_field(lds_rows, arow + i, 2);
+        cp[i] = get_field(lds_rows, crow + i, 3); cq[i] = get_field(lds_rows, crow + i, 2);
+    }
+    bool am[n], cm[n];
+    for (int i = 0; i < n; ++i) { am[i] = false; cm[i] = false; }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j)
+            if (cp[j] == ap[i] && ap[i] != 0) { am[i] = true; cm[j] = true; }
+    // k-th matched quantity (zero-padded), without runtime array indexing
+    i32 av[n], cv[n], rel[n];
+#pragma unroll
+    for (int k = 0; k < n; ++k) {
+        i32 va = 0, vc = 0;
+        int ka = 0, kc = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            if (am[i]) { if (ka == k) va = aqv[i]; ++ka; }
+            if (cm[i]) { if (kc == k) vc = cq[i]; ++kc; }
+        }
+        av[k] = va;
+        cv[k] = vc;
+    }
+    for (int i = 0; i < n; ++i) rel[i] = (cv[i] >= av[i]) ? av[i] : 0;
+    int na = 0, nc = 0;
+    for (int i = 0; i < n; ++i) { na += am[i]; nc += cm[i]; }
+    int ta = 0, fa = 0, tcn = 0, fc = 0;
+    const int l = lane_id();
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        const int ra = am[i] ? ta++ : na + fa++;
+        i32 rra = 0, rrc = 0;
+#pragma unroll
+        for (int k = 0; k < n; ++k) if (k == ra) rra = rel[k];
+        const i32 nq = wsub(aqv[i], rra);
+        if (nq == 0) { if (l < 8) lds_rows[(arow + i) * 8 + l] = 0; }
+        else if (l == 0) lds_rows[(arow + i) * 8 + 2] = nq;
+        const int rc = cm[i] ? tcn++ : nc + fc++;
+#pragma unroll
+        for (int k = 0; k < n; ++k) if (k == rc) rrc = rel[k];
+        if (l == 0) lds_rows[(crow + i) * 8 + 2] = wsub(cq[i], rrc);
+    }
+    __syncthreads();
+}
+
+// MM _getActionMsgs_fixedQuant — mm_env.py:970-1118
+template <int S>
+DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, Book<S>& B, const i32* st, i32 tid,
+                        i32 action, i32 wt0, i32 wt1, i32 last_ba, i32 last_bb, i32* lds_rows, int row, ActX& x) {
+    if (tc.fixed_action_setting) action = tc.fixed_action;
+    const i32 tick = c.tick_size;
+    // best ask / bid of the book with the agent's own orders masked out
+    i32 mn = INT_MAX, mx = INT_MIN;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const i32 pa = (B.vs.v[r] && B.a.tid[r] != tid) ? B.a.p[r] : -1;
+        const i32 pb = (B.vs.v[r] && B.b.tid[r] != tid) ? B.b.p[r] : -1;
+        mn = imin_(mn, B.vs.v[r] ? (pa == -1 ? c.lob.maxint : pa) : INT_MAX);
+        mx = imax_(mx, B.vs.v[r] ? pb : INT_MIN);
+    }
+    i32 ba = wave_min(mn), bb = wave_max(mx);
+    ba = ba == c.lob.maxint ? -1 : ba;
+    const bool empty = (ba == -1) || (bb == -1);
+    ba = wmul(ifloordiv(ba, tick), tick);
+    bb = wmul(ifloordiv(bb, tick), tick);
+    if (empty) { bb = last_bb; ba = last_ba; }
+    const float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
+    const float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
+    const int ai = action < 0 ? 0 : (action > 9 ? 9 : action);
+    // offsets tables {0,1,2,3,4,0,2,5,1,0} / {0,1,2,3,4,2,0,1,5,0}; quants 1.. ,0
+    const float bo = (float)((0x0152043210ull >> (4 * ai)) & 0xF);
+    const float ao = (float)((0x0510243210ull >> (4 * ai)) & 0xF);
+    const i32 q1 = ai == 9 ? 0 : 1;
+    i32 bq = wmul(q1, tc.fixed_quant_value), aq = wmul(q1, tc.fixed_quant_value);
+    if (empty) { bq = 0; aq = 0; }
+    const float bpf = i2f(bb) - bo * hs;
+    const float apf = i2f(ba) + ao * hs;
+    const i32 bp = f2i(ffloordiv(fmaxf(bpf, 0.0f), (float)tick) * (float)tick);
+    const i32 ap = f2i(ffloordiv(fmaxf(i2f(wadd(bp, tick)), apf), (float)tick) * (float)tick);
+    i32 typ0 = 1, typ1 = 1, sd0 = 1, sd1 = -1, qq0 = bq, qq1 = aq, pp0 = bp, pp1 = ap;
+    const i32 inv = st[2];
+    const i32 lq0 = f2i(tc.auto_liquidate_alpha * i2f(imax_(wsub(0, inv), 0)));
+    const i32 lq1 = f2i(tc.auto_liquidate_alpha * i2f(imax_(inv, 0)));
+    const i32 lp0 = f2i(i2f(ba) + hs * 10.0f), lp1 = f2i(i2f(bb) - hs * 10.0f);
+    const bool liq = (tc.tenth_action_market && action == 9) ||
+                     (tc.auto_liquidate_threshold != 0 && iabs_(inv) > tc.auto_liquidate_threshold);
+    if (liq) { typ0 = typ1 = 4; sd0 = -1; sd1 = 1; qq0 = lq0; qq1 = lq1; pp0 = lp0; pp1 = lp1; }
+    const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
+    put_row(lds_rows, row, typ0, sd0, qq0, pp0, c.placeholder_order_id, tid, ta, tb);
+    put_row(lds_rows, row + 1, typ1, sd1, qq1, pp1, c.placeholder_order_id, tid, ta, tb);
+    x.bid_price = bp; x.ask_price = ap; x.bid_dist = wsub(bb, bp); x.ask_dist = wsub(ap, ba);
+    x.bid_quant = bq; x.ask_quant = aq;
+}
+
+// MM _getActionMsgs_directional_trading — mm_env.py:1810-1865
+DEV void mm_directional(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, i32 tid, i32 action, i32 wt0, i32 wt1,
+                        i32 last_ba, i32 last_bb, i32* lds_rows, int row, ActX& x) {
+    const i32 tick = c.tick_size;
+    const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
+    const int ai = action < 0 ? 0 : (action > 2 ? 2 : action);
+    const i32 bq = (ai == 1) * tc.fixed_quant_value, aq = (ai == 2) * tc.fixed_quant_value;
+    const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
+    put_row(lds_rows, row, 1, 1, bq, ba, c.placeholder_order_id, tid, ta, tb);
+    put_row(lds_rows, row + 1, 1, -1, aq, bb, c.placeholder_order_id, tid, ta, tb);
+    x.bid_price = x.ask_price = x.bid_dist = x.ask_dist = 0;
+    x.bid_quant = bq; x.ask_quant = aq;
+}
+
+// EXE _getActionMsgs_fixedQuant_extended — exec_env.py:838-932
+DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const i32* st, i32 tid, i32 action, i32 wt0,
+                 i32 wt1, i32 last_ba, i32 last_bb, i32* lds_rows, int row) {
+    const i32 tick = c.tick_size;
+    const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
+    const i32 sell = st[3];
+    i32 pl[4];
+    if (sell) {
+        pl[0] = bb;
+        pl[1] = f2i(ceilf(ffloordiv(i2f(wadd(bb, ba)) / 2.0f, (float)tick)) * (float)tick);
+        pl[2] = ba;
+        pl[3] = wadd(ba, wmul(tick, tc.n_ticks_in_book));
+    } else {
+        pl[0] = ba;
+        pl[1] = wmul(ifloordiv(ifloordiv(wadd(bb, ba), 2), tick), tick);
+        pl[2] = bb;
+        pl[3] = wsub(bb, wmul(tick, tc.n_ticks_in_book));
+    }
+    const int ai = action < 0 ? 0 : (action > 12 ? 12 : action);
+    // quant table rows: action 0 -> none; 1..12 -> level (ai-1)%4 with multiple {1,2,5}[(ai-1)/4]
+    i32 q[4] = {0, 0, 0, 0};
+    if (ai > 0) {
+        const int lvl = (ai - 1) & 3, mul = (ai - 1) >> 2;
+        q[lvl] = wmul(mul == 0 ? 1 : (mul == 1 ? 2 : 5), tc.fixed_quant_value);
+    }
+    const i32 tot = wadd(wadd(q[0], q[1]), wadd(q[2], q[3]));
+    const i32 left = wsub(st[1], st[2]);
+    if (!(tot <= left)) { q[0] = f2i(floorf(i2f(left))); q[1] = q[2] = q[3] = 0; }
+    const i32 side = wsub(1, wmul(sell, 2));
+    const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
+    for (int k = 0; k < 4; ++k) put_row(lds_rows, row + k, 1, side, q[k], pl[k], c.placeholder_order_id, tid, ta, tb);
+}
+
+// --------------------------------------------------------------- rewards
+// Per-row trade views with an optional override row (the fictional unwind
+// trade that add_trade — JaxOrderBookArrays.py:885-889 — places at the first
+// row holding any -1; the override is per agent and never stored).
+template <int S>
+struct TradeView {
+    i32 P[S], Q[S], S4[S], PT[S], AT[S];
+    bool valid[S];  // trades[:,0] >= 0 ("executed")
+};
+template <int S>
+DEV void trade_view(const Book<S>& B, TradeView<S>& V, bool use_ovr, int ovr_idx, const i32 (&ovr)[8]) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const bool o = use_ovr && (r * 64 + l == ovr_idx);
+        const i32 p = o ? ovr[0] : B.tr.f[0][r], q = o ? ovr[1] : B.tr.f[1][r];
+        const i32 s4 = o ? ovr[4] : B.tr.f[4][r], pt = o ? ovr[6] : B.tr.f[6][r], at = o ? ovr[7] : B.tr.f[7][r];
+        const bool v = B.vt.v[r] && p >= 0;
+        V.valid[r] = v;
+        V.P[r] = v ? p : 0; V.Q[r] = v ? q : 0; V.S4[r] = v ? s4 : 0; V.PT[r] = v ? pt : 0; V.AT[r] = v ? at : 0;
+    }
+}
+template <int S> DEV int first_any_neg1_trade(const Book<S>& B) {
+    bool pr[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) any |= B.tr.f[k][r] == -1;
+        pr[r] = B.vt.v[r] && any;
+    }
+    return first_true(pr, B.c.nT - 1);
+}
+
+struct StepCtx {  // wave-uniform per-step quantities shared by the rewards
+    float avg_mid, last_mid, wmid;
+    i32 last_ba, last_bb, old_last_ba, old_last_bb;  // new / old best quotes [-1]
+    i32 init0, step;
+    bool ep_done;
+};
+
+struct MMRew {
+    float reward, reward_pv, reward_spooner, end_of_ep_pv, reward_spooner_damped, reward_spooner_asym_damped,
+        reward_spooner_asym_damped2, reward_delta_pv, market_share, delta_mid, buyPnL, sellPnL, invPnL, PnL, cash,
+        inventoryValue;
+    i32 end_inventory, forced_unwind;
+};
+
+// MM get_reward — mm_env.py:2214-2673
+template <int S>
+DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const Book<S>& B, const StepCtx& X,
+                   const i32* st, i32 tid, bool excl_any, MMRew& R) {
+    const int nT = c.lob.n_trades;
+    const float tick = (float)c.tick_size;
+    const i32 ovr0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    TradeView<S> V;
+    trade_view(B, V, false, -1, ovr0);
+    const i32 inv = st[2];
+    i32 bqs = 0, sqs = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const bool mine = (tid == V.PT[r]) || (tid == V.AT[r]);
+        const i32 aQ = mine ? V.Q[r] : 0, apt = mine ? V.PT[r] : 0, aat = mine ? V.AT[r] : 0;
+        const bool buy = (aQ >= 0 && tid == apt) || (aQ < 0 && tid == aat);
+        const bool sel = (aQ < 0 && tid == apt) || (aQ >= 0 && tid == aat);
+        bqs = wadd(bqs, buy ? iabs_(aQ) : 0);
+        sqs = wadd(sqs, sel ? iabs_(aQ) : 0);
+    }
+    bqs = wave_sum(bqs);
+    sqs = wave_sum(sqs);
+    const i32 inv_b = wsub(wadd(inv, bqs), sqs);
+    const i32 M = c.n_msgs;
+    i32 pen = wmul(tc.unwind_price_penalty, c.tick_size);
+    pen = inv_b > 0 ? pen : wsub(0, pen);
+    i32 unwind_px;
+    if (tc.unwind_price == HFTLOB_PRICE_FAR_TOUCH) unwind_px = wsub(inv_b > 0 ? X.last_bb : X.last_ba, pen);
+    else unwind_px = f2i((tc.unwind_price == HFTLOB_PRICE_MID_AVG ? X.avg_mid : X.last_mid) - i2f(pen));
+    const bool add = X.ep_done && iabs_(inv_b) > 0;
+    const i32 ovr[8] = {unwind_px, wmul(isign(inv_b), iabs_(inv_b)), c.artificial_order_id, c.placeholder_order_id,
+                        0, 0, c.artificial_trader_id, tid};
+    const int e = add ? first_any_neg1_trade(B) : -1;
+    trade_view(B, V, add, e, ovr);
+    R.forced_unwind = wmul(inv_b, (i32)X.ep_done);
+    // post-unwind stats
+    const int ri = tc.reference_price;
+    const bool ref_int = ri == HFTLOB_PRICE_FAR_TOUCH || ri == HFTLOB_PRICE_NEAR_TOUCH;
+    i32 bq = 0, sq = 0, oq = 0;
+    float inc[S], out[S], rb[S], rsl[S];
+    i32 bP[S], bQ[S], sP[S], sQ[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const bool mine = (tid == V.PT[r]) || (tid == V.AT[r]);
+        const i32 aP = mine ? V.P[r] : 0, aQ = mine ? V.Q[r] : 0, apt = mine ? V.PT[r] : 0, aat = mine ? V.AT[r] : 0;
+        oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
+        const bool buy = (aQ >= 0 && tid == apt) || (aQ < 0 && tid == aat);
+        const bool sel = (aQ < 0 && tid == apt) || (aQ >= 0 && tid == aat);
+        const bool pbuy = (aQ >= 0 && tid == apt), psel = (aQ < 0 && tid == apt);
+        bP[r] = buy ? aP : 0; bQ[r] = buy ? aQ : 0; sP[r] = sel ? aP : 0; sQ[r] = sel ? aQ : 0;
+        const i32 pbP = pbuy ? aP : 0, pbQ = pbuy ? aQ : 0, psP = psel ? aP : 0, psQ = psel ? aQ : 0;
+        bq = wadd(bq, iabs_(bQ[r]));
+        sq = wadd(sq, iabs_(sQ[r]));
+        inc[r] = i2f(sP[r]) / tick * i2f(iabs_(sQ[r]));
+        out[r] = i2f(bP[r]) / tick * i2f(iabs_(bQ[r]));
+        rb[r] = i2f(pbP) / tick * i2f(iabs_(pbQ));
+        rsl[r] = i2f(psP) / tick * i2f(iabs_(psQ));
+    }
+    bq = wave_sum(bq); sq = wave_sum(sq); oq = wave_sum(oq);
+    const float income = rows_fsum(inc, nT), outgoing = rows_fsum(out, nT);
+    const i32 new_inv = wsub(wadd(inv, bq), sq);
+    const float rebate_value = rows_fsum(rb, nT) + rows_fsum(rsl, nT);
+    const float rebate_income = rebate_value * tc.rebate_factor;
+    float ref_buy, ref_sell, ref;
+    i32 rbi = 0, rsi = 0, refi = 0;
+    if (ri == HFTLOB_PRICE_MID_AVG) { ref_buy = ref_sell = ref = X.avg_mid; }
+    else if (ref_int) {
+        const bool far = ri == HFTLOB_PRICE_FAR_TOUCH;
+        rbi = far ? X.last_ba : X.last_bb;
+        rsi = far ? X.last_bb : X.last_ba;
+        refi = new_inv > 0 ? rbi : rsi;
+        ref_buy = i2f(rbi); ref_sell = i2f(rsi); ref = i2f(refi);
+    } else { ref_buy = ref_sell = ref = X.last_mid; }
+    const float PnL = income - outgoing + rebate_income;
+    const float cash = bitf(st[4]) + PnL;
+    const float inv_value = ref_int ? i2f(wmul(new_inv, refi)) / tick : i2f(new_inv) * ref / tick;
+    const float net_worth = cash + inv_value;
+    const i32 traded = wadd(bq, sq);
+    const float market_share = i2f(traded) / i2f(wadd(traded, oq));
+    const float mid_end = X.last_mid;
+    const float invPnL = i2f(inv) * (mid_end - X.wmid) / tick;
+    float bpl[S], spl[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        if (ref_int) {
+            bpl[r] = i2f(wsub(rbi, bP[r])) / tick * i2f(iabs_(bQ[r]));
+            spl[r] = i2f(wsub(sP[r], rsi)) / tick * i2f(iabs_(sQ[r]));
+        } else {
+            bpl[r] = (ref_buy - i2f(bP[r])) / tick * i2f(iabs_(bQ[r]));
+            spl[r] = (i2f(sP[r]) - ref_sell) / tick * i2f(iabs_(sQ[r]));
+        }
+    }
+    const float buyPnL = rows_fsum(bpl, nT), sellPnL = rows_fsum(spl, nT);
+    const float eta = tc.inventoryPnL_eta, gam = tc.inventoryPnL_gamma;
+    const float r_sp = buyPnL + sellPnL + rebate_income + invPnL;
+    const float r_spd = buyPnL + sellPnL + rebate_income + invPnL - eta * invPnL;
+    const float r_spad = buyPnL + sellPnL + rebate_income + invPnL - fmaxf(0.0f, eta * invPnL);
+    const float r_spad2 = buyPnL + sellPnL + rebate_income + gam * (invPnL - fmaxf(0.0f, eta * invPnL));
+    const float r_sps = buyPnL + sellPnL + rebate_income + eta * (invPnL - tc.one_minus_eta * fmaxf(0.0f, invPnL));
+    float r_complex = 0.0f;
+    if (tc.reward_function == HFTLOB_MM_REW_COMPLEX) {
+        float abp[S], asp[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            abp[r] = i2f(bP[r]) / i2f(bq) * i2f(iabs_(bQ[r]));
+            asp[r] = i2f(sP[r]) / i2f(sq) * i2f(iabs_(sQ[r]));
+        }
+        const float avg_buy = bq > 0 ? rows_fsum(abp, nT) : 0.0f;
+        const float avg_sell = sq > 0 ? rows_fsum(asp, nT) : 0.0f;
+        const i32 inv_change = wsub(bq, sq);
+        const float real_pnl = i2f(imin_(bq, sq)) * (avg_sell - avg_buy);
+        const float unreal = inv_change > 0 ? i2f(inv_change) * (X.avg_mid - avg_buy)
+                                            : i2f(iabs_(inv_change)) * (avg_sell - X.avg_mid);
+        r_complex = real_pnl + tc.unrealizedPnL_lambda * unreal + eta * fminf(invPnL, invPnL * eta);
+    }
+    const float r_pv = i2f(new_inv) * (ref / tick) + cash;
+    float old_ref;
+    if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(inv > 0 ? X.old_last_ba : X.old_last_bb);
+    else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(inv > 0 ? X.old_last_bb : X.old_last_ba);
+    else old_ref = X.wmid;
+    const float old_nw = old_ref / tick * i2f(inv) + bitf(st[4]);
+    const float d_nw = net_worth - old_nw;
+    float reward;
+    switch (tc.reward_function) {
+        case HFTLOB_MM_REW_PORTFOLIO_VALUE: reward = r_pv; break;
+        case HFTLOB_MM_REW_BUY_SELL_PNL: reward = buyPnL + sellPnL; break;
+        case HFTLOB_MM_REW_COMPLEX: reward = r_complex; break;
+        case HFTLOB_MM_REW_ZERO_INV: reward = i2f(wsub(0, iabs_(new_inv))); break;
+        case HFTLOB_MM_REW_SPOONER: reward = r_sp; break;
+        case HFTLOB_MM_REW_SPOONER_DAMPED: reward = r_spd; break;
+        case HFTLOB_MM_REW_SPOONER_ASYM_DAMPED: reward = r_spad; break;
+        case HFTLOB_MM_REW_SPOONER_SCALED: reward = r_sps; break;
+        case HFTLOB_MM_REW_DELTA_PORTFOLIO_VALUE: reward = d_nw; break;
+        default: reward = r_spad2; break;
+    }
+    float inv_pen = 0.0f;
+    if (tc.inv_penalty == HFTLOB_INVPEN_LINEAR) inv_pen = i2f(wsub(0, iabs_(new_inv)));
+    else if (tc.inv_penalty == HFTLOB_INVPEN_QUADRATIC)
+        inv_pen = i2f(wmul(-1, wmul(new_inv, new_inv))) / tc.inv_penalty_quadratic_factor;
+    else if (tc.inv_penalty == HFTLOB_INVPEN_THRESHOLD)
+        inv_pen = i2f(iabs_(new_inv)) > tc.inv_penalty_threshold
+                      ? -1.0f * (i2f(wmul(new_inv, new_inv)) / tc.inv_penalty_quadratic_factor) : 0.0f;
+    reward = reward + tc.inv_penalty_lambda * inv_pen;
+    if (tc.clip_reward) reward = fminf(fmaxf(reward, -10000.0f), 10000.0f);
+    if (tc.volume_traded_bonus == 1) reward = reward + fabsf(reward) * market_share;
+    if (tc.exclude_extreme_spreads && excl_any) reward = 0.0f;
+    R.reward = reward; R.reward_pv = r_pv; R.reward_spooner = r_sp; R.end_of_ep_pv = r_pv * (float)X.ep_done;
+    R.reward_spooner_damped = r_spd; R.reward_spooner_asym_damped = r_spad; R.reward_spooner_asym_damped2 = r_spad2;
+    R.reward_delta_pv = d_nw; R.market_share = market_share; R.delta_mid = mid_end - X.wmid; R.buyPnL = buyPnL;
+    R.sellPnL = sellPnL; R.invPnL = invPnL; R.PnL = PnL; R.cash = cash; R.inventoryValue = inv_value;
+    R.end_inventory = new_inv;
+    (void)M;
+}
+
+struct EXRew {
+    float reward, reward_info, p_vwap, vwap_rm, price_adv_rm, slippage_rm, price_drift_rm, advantage, drift, slippage,
+        trade_duration;
+    i32 agentQuant, qp_agent, doom_quant, quant_left;
+};
+
+// EXE get_reward — exec_env.py:1511-1762
+template <int S>
+DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const Book<S>& B, const StepCtx& X,
+                    const i32* st, i32 tid, EXRew& R) {
+    const int nT = c.lob.n_trades;
+    const i32 tick = c.tick_size;
+    const i32 ovr0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    TradeView<S> V;
+    trade_view(B, V, false, -1, ovr0);
+    const i32 task = st[1], qe = st[2], sell = st[3];
+    const float init_price = bitf(st[0]);
+    i32 qsum = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) qsum = wadd(qsum, (tid == V.PT[r] || tid == V.AT[r]) ? V.Q[r] : 0);
+    const i32 qets = iabs_(wave_sum(qsum));
+    const i32 quant_left = wsub(task, wadd(qe, qets));
+    const i32 pen = wmul(tc.doom_price_penalty, tick);
+    const i32 side_sign = wsub(wmul(sell, 2), 1);
+    i32 refp;
+    if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)
+        refp = sell ? wmul(ifloordiv(wsub(X.last_bb, pen), tick), tick)
+                    : wmul(ifloordiv(wadd(X.last_ba, pen), tick), tick);
+    else
+        refp = sell ? f2i(ffloordiv(X.avg_mid - i2f(pen), (float)tick) * (float)tick)
+                    : f2i(ffloordiv(X.avg_mid + i2f(pen), (float)tick) * (float)tick);
+    const bool add = X.ep_done && quant_left > 0;
+    const i32 ovr[8] = {refp, wmul(side_sign, iabs_(quant_left)), c.artificial_order_id, c.placeholder_order_id,
+                        0, 0, c.artificial_trader_id, tid};
+    const int e = add ? first_any_neg1_trade(B) : -1;
+    trade_view(B, V, add, e, ovr);
+    R.doom_quant = wmul((i32)X.ep_done, quant_left);
+    i32 aq = 0, oq = 0, qp = 0;
+    float dur[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const bool mine = V.valid[r] && (tid == V.PT[r] || tid == V.AT[r]);
+        aq = wadd(aq, mine ? iabs_(V.Q[r]) : 0);
+        oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
+        qp = wadd(qp, mine ? wmul(ifloordiv(V.P[r], tick), iabs_(V.Q[r])) : 0);
+        dur[r] = mine ? i2f(iabs_(V.Q[r])) / i2f(task) * i2f(wsub(V.S4[r], X.init0))
+                      : i2f(0) / i2f(task) * i2f(wsub(0, X.init0));
+    }
+    aq = wave_sum(aq); oq = wave_sum(oq); qp = wave_sum(qp);
+    float pv;
+    if (oq == 0) pv = ffloordiv(X.avg_mid, (float)tick);
+    else {
+        float vw[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const bool other = V.valid[r] && !(tid == V.PT[r] || tid == V.AT[r]);
+            const i32 P = other ? V.P[r] : 0, Q = other ? V.Q[r] : 0;
+            vw[r] = i2f(ifloordiv(P, tick)) * (i2f(iabs_(Q)) / i2f(oq));
+        }
+        pv = rows_fsum(vw, nT);
+    }
+    const i32 dirs = isign(wsub(wmul(sell, 2), 1));
+    const float adv = i2f(dirs) * (i2f(qp) - pv * i2f(aq));
+    const float drift = i2f(wmul(dirs, aq)) * (pv - ffloordiv(init_price, (float)tick));
+    const float padv = adv / (i2f(aq) + 1e-9f);
+    const float pdrift = drift / (i2f(aq) + 1e-9f);
+    const float slip = adv + drift;
+    const float scf = i2f(X.step), sc1 = i2f(wadd(X.step, 1));
+    R.vwap_rm = (bitf(st[11]) * scf + pv) / sc1;
+    R.price_adv_rm = (bitf(st[9]) * scf + padv) / sc1;
+    R.slippage_rm = (bitf(st[8]) * scf + slip) / sc1;
+    R.price_drift_rm = (bitf(st[10]) * scf + pdrift) / sc1;
+    float reward = adv + tc.reward_lambda * drift;
+    R.trade_duration = bitf(st[12]) + rows_fsum(dur, nT);
+    R.quant_left = wsub(wsub(task, qe), aq);
+    R.reward_info = reward;
+    if (tc.reward_function == HFTLOB_EXE_REW_FINISH_FAST) reward = i2f(wsub(0, iabs_(R.quant_left)));
+    R.reward = reward; R.p_vwap = pv; R.advantage = adv; R.drift = drift; R.slippage = slip;
+    R.agentQuant = aq; R.qp_agent = qp;
+}
+
+// ====================================================== K2: fused env step
+// MARLEnv.step — marl_env.py:775-804 (step_env :211-709, auto-reset select)
+#define MAX_AGENT_ROWS 128
+template <int S>
+__global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
+                                                 const i32* __restrict__ actions, const i32* __restrict__ msg_data,
+                                                 const i32* __restrict__ init_states, i32* __restrict__ state,
+                                                 float* __restrict__ obs_out, float* __restrict__ rew_out,
+                                                 i32* __restrict__ done_all_out, i32* __restrict__ dones_out,
+                                                 i32* __restrict__ info_out) {
+    __shared__ __attribute__((aligned(16))) i32 rows[MAX_AGENT_ROWS * 8];
+    __shared__ i32 axs[HFTLOB_MAX_AGENTS * 6];  // per-agent action extras
+    const int e = blockIdx.x;
+    if (e >= n_env) return;
+    const int l = lane_id();
+    const bool part = c.prng_partitionable;
+    const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
+    i32* rec = state + (size_t)e * c.rec_words;
+    Book<S> B;
+    B.c = lobcfg(c.lob);
+    B.vs.init(B.c.nO);
+    B.vt.init(B.c.nT);
+    const Key key{keys[2 * e], keys[2 * e + 1]};
+    const Key k1 = split_key(key, 2, 0, part), key_reset = split_key(key, 2, 1, part);
+    // loaded / world scalars (wave-uniform)
+    const i32* Lr = rec + c.off_loaded;
+    const i32* Wr = rec + c.off_world;
+    const i32 ld_t0 = Lr[LD_T0], win = Lr[LD_WIN], max_steps = Lr[LD_MAXS], start_index = Lr[LD_START],
+              step = Lr[LD_STEP];
+    const i32 wt0 = Wr[W_T0], wt1 = Wr[W_T1], oidc = Wr[W_OIDC];
+    const float wmid = bitf(Wr[W_MID]);
+    const i32 old_last_ba = rec[c.off_best_asks + (M - 1) * 2], old_last_bb = rec[c.off_best_bids + (M - 1) * 2];
+    bool excl_any = false;
+    for (int t = 0; t < c.n_types; ++t) {
+        if (c.types[t].kind == HFTLOB_AGENT_MM && c.types[t].exclude_extreme_spreads) {
+            bool any = false;
+            for (int m = l; m < M; m += 64) {
+                const i32 pa = rec[c.off_best_asks + m * 2], pb = rec[c.off_best_bids + m * 2];
+                any |= (i2f(wsub(pa, pb)) / (i2f(wadd(pa, pb)) / 2.0f)) > 0.1f;
+            }
+            excl_any = ballot(any) != 0ull;
+        }
+    }
+    load_side(B.a, rec + c.off_asks, B.vs);
+    load_side(B.b, rec + c.off_bids, B.vs);
+
+    // ---- (C) agent messages -> LDS rows [cancels C][actions A]
+    {
+        int ag = 0, arow = C, crow = 0;
+        const i32* st = rec + c.off_agents;
+        for (int t = 0; t < c.n_types; ++t) {
+            const hftlob_agent_type_cfg& tc = c.types[t];
+            for (int i = 0; i < tc.n_agents; ++i, ++ag) {
+                const i32 tid = wsub(tc.trader_id0, i);
+                const i32 act = actions[(size_t)e * c.n_agents + ag];
+                i32 s4[4] = {st[0], st[1], st[2], st[3]};
+                ActX x{0, 0, 0, 0, 0, 0};
+                if (tc.kind == HFTLOB_AGENT_MM) {
+                    if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
+                        mm_directional(c, tc, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
+                    else
+                        mm_fixed_quant(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
+                    const int sz = tc.n_msgs / 4;
+                    cancel_rows(B.b, B.vs, tid, sz, 1, wt0, wt1, rows, crow);
+                    cancel_rows(B.a, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
+                } else {
+                    exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow);
+                    const i32 sell = s4[3];
+                    cancel_rows(sell ? B.a : B.b, B.vs, tid, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
+                                crow);
+                }
+                {
+                    const i32 xv[6] = {x.bid_price, x.ask_price, x.bid_dist, x.ask_dist, x.bid_quant, x.ask_quant};
+                    i32 v = 0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) if (l == k) v = xv[k];
+                    if (l < 6) axs[ag * 6 + l] = v;
+                }
+                if (tc.kind == HFTLOB_AGENT_MM) filter_rows<2>(rows, arow, crow);
+                else filter_rows<4>(rows, arow, crow);
+                arow += tc.n_action_msgs;
+                crow += tc.n_msgs - tc.n_action_msgs;
+                st += agent_words(tc);
+            }
+        }
+    }
+    __syncthreads();
+    // order ids (counter - j) and the action-row permutation (lane j = action row j)
+    {
+        i32 f[8];
+        const bool act_lane = l < A;
+        if (act_lane) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) f[k] = rows[(C + l) * 8 + k];
+            f[4] = wsub(oidc, l);
+        }
+        int dest = l;
+        if (c.shuffle_action_messages && A >= 2) {
+            const Key sk = split_key(k1, 2, 1, part);
+            const Key sub = split_key(sk, 2, 1, part);
+            const u32 bits = random_bits(sub, A, l, part);
+            int rank = 0;
+            for (int j = 0; j < A; ++j) {
+                const u32 bj = (u32)rdl((i32)bits, j);
+                rank += (bj < bits) || (bj == bits && j < l);
+            }
+            dest = rank;
+        }
+        __syncthreads();
+        if (act_lane) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rows[(C + dest) * 8 + k] = f[k];
+        }
+        __syncthreads();
+    }
+
+    // ---- (B)+(D) stream the combined messages through the book, 64 per chunk
+    trades_fill(B.tr, -1);
+    i32 dstart = wadd(start_index, wmul(D, step));
+    dstart = imax_(0, imin_(dstart, c.n_data_rows - D));  // dynamic_slice clamping
+    const int AR = C + A;
+    bool abort_any = false;
+    i32 prev_a = -1, prev_b = -1;
+    float mid_acc = 0.0f, pa_acc = 0.0f, pb_acc = 0.0f;
+    i32 last_p_a = 0, last_p_b = 0, last_t0 = 0, last_t1 = 0;
+    for (int base = 0; base < M; base += 64) {
+        const int row = base + l;
+        int4 x = make_int4(0, 0, 0, 0), y = x;
+        if (row < AR) {
+            x = reinterpret_cast<const int4*>(rows + row * 8)[0];
+            y = reinterpret_cast<const int4*>(rows + row * 8)[1];
+        } else if (row < M) {
+            const i32* g = msg_data + (size_t)(dstart + row - AR) * 8;
+            x = reinterpret_cast<const int4*>(g)[0];
+            y = reinterpret_cast<const int4*>(g)[1];
+        }
+        i32 cap = 0, caq = 0, cbp = 0, cbq = 0;
+        const int cnt = imin_(64, M - base);
+        for (int k = 0; k < cnt; ++k) {
+            process_msg(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k), rdl(y.z, k),
+                        rdl(y.w, k));
+            refresh_best(B);
+            // abort flag on raw quotes; _ffill_best_prices (marl_env.py:723-749) on the fly
+            i32 pa = B.a.best_p, qa = B.a.best_q, pb = B.b.best_p, qb = B.b.best_q;
+            abort_any |= (pa == -1) || (pb == -1);
+            if (base + k == 0) {
+                if (pa == -1) { pa = old_last_ba; qa = 0; }
+                if (pb == -1) { pb = old_last_bb; qb = 0; }
+            }
+            if (pa == -1) qa = 0;
+            if (pb == -1) qb = 0;
+            if (pa != -1) prev_a = pa;
+            if (pb != -1) prev_b = pb;
+            cap = wrl(cap, prev_a, k); caq = wrl(caq, qa, k);
+            cbp = wrl(cbp, prev_b, k); cbq = wrl(cbq, qb, k);
+        }
+        if (row < M) {
+            reinterpret_cast<int2*>(rec + c.off_best_asks)[row] = make_int2(cap, caq);
+            reinterpret_cast<int2*>(rec + c.off_best_bids)[row] = make_int2(cbp, cbq);
+            const float mf = i2f(wadd(cbp, cap)) / 2.0f;
+            mid_acc = base == 0 ? mf : mid_acc + mf;
+            pa_acc = base == 0 ? i2f(cap) : pa_acc + i2f(cap);
+            pb_acc = base == 0 ? i2f(cbp) : pb_acc + i2f(cbp);
+        }
+        if (base + 64 >= M) {  // final time = last combined row's (s, ns)
+            last_t0 = rdl(y.z, cnt - 1);
+            last_t1 = rdl(y.w, cnt - 1);
+        }
+    }
+    last_p_a = prev_a;
+    last_p_b = prev_b;
+    StepCtx X;
+    X.avg_mid = wave_fsum(mid_acc) / (float)M;
+    X.last_ba = last_p_a; X.last_bb = last_p_b;
+    X.last_mid = i2f(wadd(last_p_b, last_p_a)) / 2.0f;
+    X.wmid = wmid;
+    X.old_last_ba = old_last_ba; X.old_last_bb = old_last_bb;
+    X.init0 = ld_t0; X.step = step;
+    X.ep_done = wsub(wsub(max_steps, step), 1) <= 1;
+    const bool all = X.ep_done;
+
+    // ---- (E) rewards, (G) agent states, (K) observations
+    WorldView wv;
+    wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
+    wv.vol_a = side_volume(B.a, B.vs); wv.vol_b = side_volume(B.b, B.vs);
+    wv.step = wadd(step, 1); wv.max_steps = max_steps; wv.mid = X.last_mid;
+    i32* info = info_out ? info_out + (size_t)e * c.info_words : nullptr;
+    {
+        int ag = 0;
+        i32* st = rec + c.off_agents;
+        for (int t = 0; t < c.n_types; ++t) {
+            const hftlob_agent_type_cfg& tc = c.types[t];
+            for (int i = 0; i < tc.n_agents; ++i, ++ag) {
+                const i32 tid = wsub(tc.trader_id0, i);
+                const int nw = agent_words(tc);
+                i32 s[13];
+                for (int k = 0; k < 13; ++k) s[k] = k < nw ? st[k] : 0;
+                i32 d = 0;
+                float rew;
+                i32 iw[HFTLOB_INFO_AGENT_WORDS];
+                for (int k = 0; k < HFTLOB_INFO_AGENT_WORDS; ++k) iw[k] = 0;
+                ActX ax1;
+                ax1.bid_price = uni(axs[ag * 6 + 0]); ax1.ask_price = uni(axs[ag * 6 + 1]);
+                ax1.bid_dist = uni(axs[ag * 6 + 2]); ax1.ask_dist = uni(axs[ag * 6 + 3]);
+                ax1.bid_quant = uni(axs[ag * 6 + 4]); ax1.ask_quant = uni(axs[ag * 6 + 5]);
+                if (tc.kind == HFTLOB_AGENT_MM) {
+                    MMRew R;
+                    mm_reward(c, tc, B, X, s, tid, excl_any, R);
+                    const float tot = bitf(s[3]) + R.PnL;
+                    s[0] = ax1.bid_dist; s[1] = ax1.ask_dist; s[2] = R.end_inventory; s[3] = fbit(tot);
+                    s[4] = fbit(R.cash);
+                    rew = R.reward / tc.reward_scaling_quo;
+                    iw[0] = fbit(R.reward); iw[1] = fbit(R.reward_pv); iw[2] = fbit(R.reward_spooner);
+                    iw[3] = fbit(R.end_of_ep_pv); iw[4] = fbit(R.reward_spooner_damped);
+                    iw[5] = fbit(R.reward_spooner_asym_damped); iw[6] = fbit(R.reward_spooner_asym_damped2);
+                    iw[7] = fbit(R.reward_delta_pv); iw[8] = fbit(tot); iw[9] = 0; iw[10] = s[2];
+                    iw[11] = fbit(R.delta_mid); iw[12] = fbit(R.market_share); iw[13] = fbit(R.buyPnL);
+                    iw[14] = R.forced_unwind; iw[15] = fbit(R.invPnL); iw[16] = ax1.bid_price;
+                    iw[17] = ax1.ask_price; iw[18] = ax1.bid_dist; iw[19] = ax1.ask_dist;
+                    iw[20] = ax1.ask_quant; iw[21] = ax1.bid_quant; iw[22] = fbit(R.sellPnL);
+                    iw[23] = fbit(R.inventoryValue);
+                } else {
+                    EXRew R;
+                    exe_reward(c, tc, B, X, s, tid, R);
+                    s[2] = wadd(s[2], R.agentQuant);
+                    s[4] = fbit(R.p_vwap);
+                    s[5] = fbit(bitf(s[5]) + i2f(R.qp_agent));
+                    s[6] = fbit(bitf(s[6]) + R.drift);
+                    s[7] = fbit(bitf(s[7]) + R.advantage);
+                    s[8] = fbit(R.slippage_rm); s[9] = fbit(R.price_adv_rm); s[10] = fbit(R.price_drift_rm);
+                    s[11] = fbit(R.vwap_rm); s[12] = fbit(R.trade_duration);
+                    d = wsub(s[1], s[2]) <= 0;
+                    rew = R.reward / tc.reward_scaling_quo;
+                    iw[0] = R.quant_left; iw[1] = d; iw[2] = fbit(R.slippage); iw[3] = fbit(R.vwap_rm);
+                    iw[4] = fbit(R.drift); iw[5] = fbit(R.advantage); iw[6] = R.doom_quant; iw[7] = s[3];
+                    iw[8] = fbit(R.reward_info);
+                }
+                if (l == 0) {
+                    rew_out[(size_t)e * c.n_agents + ag] = rew;
+                    dones_out[(size_t)e * c.n_agents + ag] = d;
+                }
+                if (info) {
+                    i32 v = 0;
+                    for (int k = 0; k < HFTLOB_INFO_AGENT_WORDS; ++k) if (l == k) v = iw[k];
+                    if (l < HFTLOB_INFO_AGENT_WORDS) info[HFTLOB_INFO_WORLD_WORDS + ag * HFTLOB_INFO_AGENT_WORDS + l] = v;
+                }
+                if (!all) {  // stepped state + obs survive only when the episode continues
+                    i32 v = 0;
+                    for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
+                    if (l < nw) st[l] = v;
+                    write_obs(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0);
+                }
+                st += nw;
+            }
+        }
+    }
+    // ---- (F) world state + info
+    const float new_mid = X.last_mid;
+    const float dt = i2f(last_t0) + i2f(last_t1) / 1e9f - i2f(wt0) - i2f(wt1) / 1e9f;
+    if (info) {
+        const float ava = wave_fsum(pa_acc) / (float)M, avb = wave_fsum(pb_acc) / (float)M;
+        i32 wv_[HFTLOB_INFO_WORLD_WORDS] = {win, fbit(new_mid), wadd(step, 1), last_t0, last_t1, wsub(oidc, A),
+                                            last_p_a, last_p_b, fbit(ava), fbit(avb), fbit(dt), (i32)X.ep_done,
+                                            (i32)abort_any, wsub(last_p_a, last_p_b)};
+        i32 v = 0;
+        for (int k = 0; k < HFTLOB_INFO_WORLD_WORDS; ++k) if (l == k) v = wv_[k];
+        if (l < HFTLOB_INFO_WORLD_WORDS) info[l] = v;
+    }
+    if (l == 0) done_all_out[e] = all;
+    if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
+        env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt);
+        return;
+    }
+    store_side(B.a, rec + c.off_asks, B.vs);
+    store_side(B.b, rec + c.off_bids, B.vs);
+    store_trades(B.tr, rec + c.off_trades, B.vt);
+    if (l == 0) {
+        rec[c.off_loaded + LD_STEP] = wadd(step, 1);
+        i32* W = rec + c.off_world;
+        W[W_T0] = last_t0; W[W_T1] = last_t1; W[W_OIDC] = wsub(oidc, A); W[W_MID] = fbit(new_mid); W[W_DT] = fbit(dt);
+    }
+}
+
+// ==================================================== K3/K4: PRNG kernels
+__global__ void k_sample_actions(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys, i32* __restrict__ actions) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_env) return;
+    const bool part = c.prng_partitionable;
+    const Key k{keys[2 * e], keys[2 * e + 1]};
+    int a = 0;
+    for (int t = 0; t < c.n_types; ++t) {
+        const Key sub = split_key(k, c.n_types, t, part);
+        for (int i = 0; i < c.types[t].n_agents; ++i, ++a)
+            actions[(size_t)e * c.n_agents + a] =
+                randint(split_key(sub, c.types[t].n_agents, i, part), 0, c.types[t].n_actions, part);
+    }
+}
+__global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__ keys, u32* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_env * n) return;
+    const int e = t / n, j = t % n;
+    const Key o = split_key(Key{keys[2 * e], keys[2 * e + 1]}, n, j, part != 0);
+    out[2 * (size_t)t] = o.a;
+    out[2 * (size_t)t + 1] = o.b;
+}
+
+// ================================================================ C ABI
+static thread_local char g_err[256] = "";
+static int fail(int code, const char* msg) {
+    snprintf(g_err, sizeof g_err, "%s", msg);
+    return code;
+}
+static int slot_sets(int n) { return n <= 64 ? 1 : (n <= 128 ? 2 : 4); }
+
+extern "C" {
+
+int hftlob_version(void) { return HFTLOB_ABI_VERSION; }
+const char* hftlob_last_error(void) { return g_err; }
+
+static int check_lob(const hftlob_lob_cfg* c) {
+    if (!c) return fail(HFTLOB_ENULL, "null cfg");
+    if (c->cancel_mode < 0 || c->cancel_mode > 1) return fail(HFTLOB_EINVAL, "cancel_mode 2/3 (random cancel) unsupported");
+    if (c->type_4_interpretation < 0 || c->type_4_interpretation > 2) return fail(HFTLOB_EINVAL, "bad type_4_interpretation");
+    if (c->n_orders < 1 || c->n_orders > HFTLOB_MAX_SLOTS || c->n_trades < 1 || c->n_trades > HFTLOB_MAX_SLOTS)
+        return fail(HFTLOB_ESHAPE, "n_orders / n_trades out of range");
+    return HFTLOB_OK;
+}
+static int launch_status() {
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return fail(HFTLOB_ELAUNCH, hipGetErrorString(err));
+    return HFTLOB_OK;
+}
+
+int hftlob_book_process(const hftlob_lob_cfg* cfg, int n_env, int n_msg, const int32_t* msgs, int32_t* asks,
+                        int32_t* bids, int32_t* trades, int32_t* best_asks, int32_t* best_bids, void* stream) {
+    int rc = check_lob(cfg);
+    if (rc) return rc;
+    if (n_env < 0 || n_msg < 0) return fail(HFTLOB_ESHAPE, "negative size");
+    if (n_env == 0) return HFTLOB_OK;
+    if (!asks || !bids || !trades || (n_msg > 0 && !msgs)) return fail(HFTLOB_ENULL, "null array");
+    if ((best_asks == nullptr) != (best_bids == nullptr)) return fail(HFTLOB_ENULL, "best_asks/best_bids: both or none");
+    const int S = slot_sets(cfg->n_orders > cfg->n_trades ? cfg->n_orders : cfg->n_trades);
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(n_env), b(64);
+    if (S == 1) hipLaunchKernelGGL(k_book_process<1>, g, b, 0, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+    else if (S == 2) hipLaunchKernelGGL(k_book_process<2>, g, b, 0, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+    else hipLaunchKernelGGL(k_book_process<4>, g, b, 0, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+    return launch_status();
+}
+
+static int check_env(const hftlob_env_cfg* c) {
+    if (!c) return fail(HFTLOB_ENULL, "null cfg");
+    int rc = check_lob(&c->lob);
+    if (rc) return rc;
+    if (c->ep_type != 0) return fail(HFTLOB_EINVAL, "only ep_type fixed_steps is supported");
+    if (c->n_types < 1 || c->n_types > HFTLOB_MAX_TYPES || c->n_agents < 1 || c->n_agents > HFTLOB_MAX_AGENTS)
+        return fail(HFTLOB_ESHAPE, "agent counts out of range");
+    if (c->n_msgs < 1 || c->n_msgs > HFTLOB_MAX_MSGS || c->n_action_msgs > 64 ||
+        c->n_action_msgs + c->n_cancel_msgs > MAX_AGENT_ROWS)
+        return fail(HFTLOB_ESHAPE, "message counts out of range");
+    if (c->n_data_msg < 1 || c->n_data_rows < c->n_data_msg || c->n_windows < 1)
+        return fail(HFTLOB_ESHAPE, "data / window sizes out of range");
+    if (c->obs_stride > HFTLOB_MAX_OBS) return fail(HFTLOB_ESHAPE, "obs_stride too large");
+    int agents = 0;
+    for (int t = 0; t < c->n_types; ++t) {
+        const hftlob_agent_type_cfg& tc = c->types[t];
+        agents += tc.n_agents;
+        if (tc.kind == HFTLOB_AGENT_MM) {
+            if (tc.sell_buy_all_option) return fail(HFTLOB_EINVAL, "MM sell_buy_all_option unsupported");
+            if (tc.n_action_msgs != 2 || tc.n_msgs != 4) return fail(HFTLOB_EINVAL, "MM message counts");
+        } else if (tc.kind == HFTLOB_AGENT_EXE) {
+            if (tc.n_action_msgs != 4 || tc.n_msgs != 8) return fail(HFTLOB_EINVAL, "EXE message counts");
+        } else return fail(HFTLOB_EINVAL, "unknown agent kind");
+    }
+    if (agents != c->n_agents) return fail(HFTLOB_EINVAL, "n_agents mismatch");
+    return HFTLOB_OK;
+}
+
+int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const int32_t* msg_data,
+                     const int32_t* init_states, int32_t* state, const hftlob_step_out* out, void* stream) {
+    int rc = check_env(cfg);
+    if (rc) return rc;
+    (void)msg_data;
+    if (n_env < 0) return fail(HFTLOB_ESHAPE, "negative n_env");
+    if (n_env == 0) return HFTLOB_OK;
+    if (!keys || !init_states || !state) return fail(HFTLOB_ENULL, "null array");
+    float* obs = out ? out->obs : nullptr;
+    const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(n_env), b(64);
+    if (S == 1) hipLaunchKernelGGL(k_env_reset<1>, g, b, 0, st, *cfg, n_env, keys, init_states, state, obs);
+    else if (S == 2) hipLaunchKernelGGL(k_env_reset<2>, g, b, 0, st, *cfg, n_env, keys, init_states, state, obs);
+    else hipLaunchKernelGGL(k_env_reset<4>, g, b, 0, st, *cfg, n_env, keys, init_states, state, obs);
+    return launch_status();
+}
+
+int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const int32_t* actions,
+                    const int32_t* msg_data, const int32_t* init_states, int32_t* state, const hftlob_step_out* out,
+                    void* stream) {
+    int rc = check_env(cfg);
+    if (rc) return rc;
+    if (n_env < 0) return fail(HFTLOB_ESHAPE, "negative n_env");
+    if (n_env == 0) return HFTLOB_OK;
+    if (!keys || !actions || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
+    if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
+    const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(n_env), b(64);
+#define LAUNCH_STEP(SS) hipLaunchKernelGGL(k_env_step<SS>, g, b, 0, st, *cfg, n_env, keys, actions, msg_data, init_states, \
+                                           state, out->obs, out->rewards, out->done_all, out->dones, out->info)
+    if (S == 1) LAUNCH_STEP(1);
+    else if (S == 2) LAUNCH_STEP(2);
+    else LAUNCH_STEP(4);
+#undef LAUNCH_STEP
+    return launch_status();
+}
+
+int hftlob_sample_actions(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, int32_t* actions, void* stream) {
+    if (!cfg) return fail(HFTLOB_ENULL, "null cfg");
+    if (cfg->n_types < 1 || cfg->n_types > HFTLOB_MAX_TYPES) return fail(HFTLOB_ESHAPE, "n_types");
+    if (n_env < 0) return fail(HFTLOB_ESHAPE, "negative n_env");
+    if (n_env == 0) return HFTLOB_OK;
+    if (!keys || !actions) return fail(HFTLOB_ENULL, "null array");
+    hipLaunchKernelGGL(k_sample_actions, dim3((n_env + 255) / 256), dim3(256), 0, (hipStream_t)stream, *cfg, n_env, keys,
+                       actions);
+    return launch_status();
+}
+
+int hftlob_split_keys(int n_env, int n, int partitionable, const uint32_t* keys, uint32_t* out, void* stream) {
+    if (n_env < 0 || n < 1) return fail(HFTLOB_ESHAPE, "bad sizes");
+    if (n_env == 0) return HFTLOB_OK;
+    if (!keys || !out) return fail(HFTLOB_ENULL, "null array");
+    const long total = (long)n_env * n;
+    hipLaunchKernelGGL(k_split_keys, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n_env, n,
+                       partitionable, keys, out);
+    return launch_status();
+}
+
+}  // extern "C"

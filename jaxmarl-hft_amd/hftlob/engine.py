@@ -1,0 +1,90 @@
+"""Order-book engine operators (device tensors in, device tensors out).
+
+Mirrors the reference operator API of ``gymnax_exchange/jaxob/
+JaxOrderBookArrays.py`` for the batched case the MARL path uses:
+
+* ``scan_through_entire_array_save_bidask(cfg, key, msg_array, book_state,
+  N_steps)`` (:791-823) -> ``((asks, bids, trades), (best_asks[-N:],
+  best_bids[-N:]))``
+* ``scan_through_entire_array(cfg, key, msg_array, book_state)`` (:736-756)
+
+Every array carries a leading env dimension (the reference is vmapped; here
+the batch is explicit).  ``key`` is accepted for signature parity; it only
+matters for cancel modes 2/3, which are not implemented.  Functional like the
+reference: inputs are not modified.  ``book_process_`` is the in-place form.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from .config import JAXLOB_Configuration
+from .layout import pack_lob_cfg
+
+
+def _lob(cfg: JAXLOB_Configuration):
+    return pack_lob_cfg(cfg)
+
+
+def _batched(x: torch.Tensor, tail: int) -> torch.Tensor:
+    return x if x.dim() == tail + 1 else x.unsqueeze(0)
+
+
+def book_process_(cfg: JAXLOB_Configuration, msgs: torch.Tensor, asks: torch.Tensor, bids: torch.Tensor,
+                  trades: torch.Tensor, best_asks: Optional[torch.Tensor] = None,
+                  best_bids: Optional[torch.Tensor] = None, stream=None) -> None:
+    """In place: process msgs [E, M, 8] through (asks, bids [E, nO, 6], trades [E, nT, 8])."""
+    E, M = msgs.shape[0], msgs.shape[1]
+    for t, shp in ((msgs, (E, M, 8)), (asks, (E, cfg.nOrders, 6)), (bids, (E, cfg.nOrders, 6)),
+                   (trades, (E, cfg.nTrades, 8))):
+        if tuple(t.shape) != shp or t.dtype != torch.int32:
+            raise ValueError(f"expected int32 {shp}, got {t.dtype} {tuple(t.shape)}")
+    if best_asks is not None and (tuple(best_asks.shape) != (E, M, 2) or tuple(best_bids.shape) != (E, M, 2)):
+        raise ValueError("best_asks / best_bids must be int32 [E, M, 2]")
+    L = _lib.lib()
+    c = _lob(cfg)
+    _lib.check(L.hftlob_book_process(C.byref(c), E, M, _lib.ptr(msgs), _lib.ptr(asks), _lib.ptr(bids),
+                                     _lib.ptr(trades), _lib.ptr(best_asks), _lib.ptr(best_bids),
+                                     _lib.stream_ptr(stream)))
+
+
+def scan_through_entire_array_save_bidask(cfg: JAXLOB_Configuration, key, msg_array: torch.Tensor,
+                                          book_state: Tuple[torch.Tensor, torch.Tensor, torch.Tensor],
+                                          N_steps: Optional[int] = None):
+    single = msg_array.dim() == 2
+    msgs = _batched(msg_array, 2).contiguous()
+    asks, bids, trades = (_batched(x, 2).clone().contiguous() for x in book_state)
+    E, M = msgs.shape[0], msgs.shape[1]
+    ba = torch.empty((E, M, 2), dtype=torch.int32, device=msgs.device)
+    bb = torch.empty_like(ba)
+    book_process_(cfg, msgs, asks, bids, trades, ba, bb)
+    n = M if N_steps is None else N_steps
+    ba, bb = ba[:, M - n:], bb[:, M - n:]
+    if single:
+        asks, bids, trades, ba, bb = asks[0], bids[0], trades[0], ba[0], bb[0]
+    return (asks, bids, trades), (ba, bb)
+
+
+def scan_through_entire_array(cfg: JAXLOB_Configuration, key, msg_array: torch.Tensor,
+                              book_state: Tuple[torch.Tensor, torch.Tensor, torch.Tensor]):
+    single = msg_array.dim() == 2
+    msgs = _batched(msg_array, 2).contiguous()
+    asks, bids, trades = (_batched(x, 2).clone().contiguous() for x in book_state)
+    book_process_(cfg, msgs, asks, bids, trades)
+    if single:
+        return asks[0], bids[0], trades[0]
+    return asks, bids, trades
+
+
+def init_orderside(nOrders: int = 100, n_env: Optional[int] = None, device="cuda") -> torch.Tensor:
+    """init_orderside — JaxOrderBookArrays.py:987-997 (all -1)."""
+    shape = (nOrders, 6) if n_env is None else (n_env, nOrders, 6)
+    return torch.full(shape, -1, dtype=torch.int32, device=device)
+
+
+def init_trades(nTrades: int = 100, n_env: Optional[int] = None, device="cuda") -> torch.Tensor:
+    shape = (nTrades, 8) if n_env is None else (n_env, nTrades, 8)
+    return torch.full(shape, -1, dtype=torch.int32, device=device)

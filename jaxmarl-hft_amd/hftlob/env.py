@@ -1,0 +1,330 @@
+"""``MARLEnv`` — the multi-agent LOB environment on the HIP path.
+
+Drop-in for ``gymnax_exchange/jaxen/marl_env.py:MARLEnv`` (:45-804): same
+constructor arguments, ``default_params``, ``reset(key, params) -> (obs_list,
+state)``, ``step(key, state, actions, params) -> (obs_list, state,
+reward_list, dones, info)``, ``action_spaces`` / ``observation_spaces``,
+``num_msgs_per_step``.  The reference is written per-env and vmapped by its
+callers (``jax.vmap(env.step, in_axes=(0,0,0,None))``); here the env batch
+is explicit: ``key`` is uint32 ``[E, 2]``, every state leaf / action / output
+carries a leading ``E``.  One ``step`` is ONE kernel launch
+(``hftlob_env_step``) over all envs, auto-reset included.
+
+State lives in one int32 tensor ``[E, rec_words]`` (see ``layout.py``);
+``MultiAgentState.world_state`` / ``.agent_states`` expose the reference's
+pytree field names as zero-copy views.  ``step`` updates the state in place
+and returns the same object (callers that rebind ``state = step(...)[1]``, as
+every reference caller does, see no difference).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import MarketMaking_EnvironmentConfig, MultiAgentConfig
+from .data.synthetic import LobsterDay, generate_day
+from .data.windows import Windows, init_messages, loaded_rows, make_windows
+from .engine import book_process_
+from .layout import (AGENT_MM, EXE_FLOAT, EXE_WORDS, INFO_AGENT_WORDS, INFO_EXE, INFO_MM, INFO_WORLD,
+                     INFO_WORLD_WORDS, MM_FLOAT, MM_WORDS, EnvLayout, StepOut, pack_env_cfg, trader_ids)
+
+
+# ------------------------------------------------------------------ spaces
+class Discrete:
+    def __init__(self, n: int):
+        self.n, self.shape, self.dtype = int(n), (), torch.int32
+
+
+class Box:
+    def __init__(self, low, high, shape, dtype=torch.float32):
+        self.low, self.high, self.shape, self.dtype = low, high, tuple(shape), dtype
+
+
+# ------------------------------------------------------------------ params
+@dataclass
+class LoadedEnvParams:               # StatesandParams.py:96-101
+    message_data: torch.Tensor       # (N, 8) int32
+    book_data: torch.Tensor          # (W, 40) int32
+    init_states_array: torch.Tensor  # (W, init_rec_words) int32
+
+
+@dataclass
+class MMEnvParams:                   # StatesandParams.py:111-116
+    trader_id: torch.Tensor
+    time_delay_obs_act: torch.Tensor
+    normalize: torch.Tensor
+
+
+@dataclass
+class ExecEnvParams:                 # StatesandParams.py:119-124
+    trader_id: torch.Tensor
+    task_size: torch.Tensor
+    reward_lambda: torch.Tensor
+    time_delay_obs_act: torch.Tensor
+    normalize: torch.Tensor
+
+
+@dataclass
+class MultiAgentParams:              # StatesandParams.py:104-108
+    loaded_params: LoadedEnvParams
+    agent_params: list
+
+
+# ------------------------------------------------------------------- state
+def _iview(buf, off, shape):
+    n = int(np.prod(shape)) if shape else 1
+    v = buf[:, off:off + n]
+    return v.reshape(buf.shape[0], *shape) if shape else v[:, 0]
+
+
+class WorldState:
+    """Views of the world part of the record (WorldState, StatesandParams.py:29-38)."""
+
+    def __init__(self, buf: torch.Tensor, L: EnvLayout):
+        self._buf, self._L = buf, L
+
+    def __getattr__(self, name):
+        b, L = self.__dict__["_buf"], self.__dict__["_L"]
+        nO, nT, M = L.n_orders, L.n_trades, L.n_msgs
+        lo, w = L.off_loaded, L.off_world
+        table = {
+            "ask_raw_orders": lambda: _iview(b, L.off_asks, (nO, 6)),
+            "bid_raw_orders": lambda: _iview(b, L.off_bids, (nO, 6)),
+            "trades": lambda: _iview(b, L.off_trades, (nT, 8)),
+            "init_time": lambda: b[:, lo:lo + 2],
+            "window_index": lambda: b[:, lo + 2],
+            "max_steps_in_episode": lambda: b[:, lo + 3],
+            "start_index": lambda: b[:, lo + 4],
+            "step_counter": lambda: b[:, lo + 5],
+            "best_bids": lambda: _iview(b, L.off_best_bids, (M, 2)),
+            "best_asks": lambda: _iview(b, L.off_best_asks, (M, 2)),
+            "time": lambda: b[:, w:w + 2],
+            "order_id_counter": lambda: b[:, w + 2],
+            "mid_price": lambda: b[:, w + 3:w + 4].view(torch.float32)[:, 0],
+            "delta_time": lambda: b[:, w + 4:w + 5].view(torch.float32)[:, 0],
+        }
+        if name not in table:
+            raise AttributeError(name)
+        return table[name]()
+
+
+class AgentStates:
+    """Per-type agent state views [E, n_agents] (MMEnvState / ExecEnvState)."""
+
+    def __init__(self, buf, offsets: List[int], kind: int):
+        self._buf, self._offs, self._kind = buf, offsets, kind
+        self._names = MM_WORDS if kind == AGENT_MM else EXE_WORDS
+
+    def __getattr__(self, name):
+        d = self.__dict__
+        if name not in d["_names"]:
+            raise AttributeError(name)
+        k = d["_names"].index(name)
+        offs, W = d["_offs"], (5 if d["_kind"] == AGENT_MM else 13)
+        o0 = offs[0] + k
+        v = d["_buf"][:, o0:o0 + W * (len(offs) - 1) + 1:W]
+        return v.view(torch.float32) if name in (MM_FLOAT if d["_kind"] == AGENT_MM else EXE_FLOAT) else v
+
+
+@dataclass
+class MultiAgentState:               # StatesandParams.py:43-47
+    buf: torch.Tensor                # (E, rec_words) int32 record
+    world_state: WorldState
+    agent_states: list
+
+    def clone(self, env: "MARLEnv") -> "MultiAgentState":
+        return env._wrap(self.buf.clone())
+
+
+# -------------------------------------------------------------------- env
+class MARLEnv:
+    def __init__(self, key, multi_agent_config: MultiAgentConfig, data: Optional[LobsterDay] = None,
+                 device=None, prng_partitionable: bool = True, return_info: bool = True,
+                 persistent_outputs: bool = False):
+        self.multi_agent_config = cfg = multi_agent_config
+        self.device = torch.device(device or "cuda")
+        w = cfg.world_config
+        self.num_agents = sum(cfg.number_of_agents_per_type)
+        self.list_of_agents_configs = list(cfg.dict_of_agents_configs.values())
+        self.type_names = [a.short_name for a in self.list_of_agents_configs]
+        if data is None:
+            data = generate_day(seed=20260403, snap_every=w.n_data_msg_per_step * w.start_resolution)
+        self.data = data
+        self.windows: Windows = make_windows(data, w)
+        self.n_windows = len(self.windows.starts)
+        self.cfg_c, self.layout = pack_env_cfg(cfg, self.n_windows, data.msgs.shape[0], prng_partitionable)
+        L = self.layout
+        self.num_msgs_per_step = L.n_msgs
+        self.num_action_msgs_per_step_by_all_agents = L.n_action_msgs
+        self.action_spaces = [Discrete(a.n_actions) for a in self.list_of_agents_configs]
+        self.observation_spaces = [Box(-1000 if isinstance(a, MarketMaking_EnvironmentConfig) else -10000,
+                                       1000 if isinstance(a, MarketMaking_EnvironmentConfig) else 10000,
+                                       (d,)) for a, d in zip(self.list_of_agents_configs, L.obs_dims)]
+        self.return_info = return_info
+        self.persistent_outputs = persistent_outputs
+        self._out = None
+        self._init_states = self._precompute_init_states()
+
+    # BaseLOBEnv._init_states (base_env.py:298-333) on the GPU engine
+    def _precompute_init_states(self) -> torch.Tensor:
+        w, L = self.multi_agent_config.world_config, self.layout
+        W, dev = self.n_windows, self.device
+        first_times = self.data.msgs[self.windows.starts, 6:8].astype(np.int32)
+        im = torch.from_numpy(init_messages(self.windows.books, first_times, w.book_depth, w.init_id)).to(dev)
+        asks = torch.full((W, w.nOrders, 6), -1, dtype=torch.int32, device=dev)
+        bids = torch.full_like(asks, -1)
+        trades = torch.full((W, w.nTrades, 8), -1, dtype=torch.int32, device=dev)
+        book_process_(w, im.contiguous(), asks, bids, trades)
+        rows = loaded_rows(asks.cpu().numpy(), bids.cpu().numpy(), trades.cpu().numpy(), first_times,
+                           self.windows, w.n_data_msg_per_step, L.init_rec_words)
+        return torch.from_numpy(rows).to(dev)
+
+    @property
+    def default_params(self) -> MultiAgentParams:
+        w = self.multi_agent_config.world_config
+        loaded = LoadedEnvParams(message_data=torch.from_numpy(self.data.msgs).to(self.device).contiguous(),
+                                 book_data=torch.from_numpy(self.windows.books).to(self.device),
+                                 init_states_array=self._init_states)
+        plist = []
+        for a, ids in zip(self.list_of_agents_configs, trader_ids(self.multi_agent_config)):
+            n = len(ids)
+            tid = torch.tensor(ids, dtype=torch.int32)
+            if isinstance(a, MarketMaking_EnvironmentConfig):
+                plist.append(MMEnvParams(tid, torch.full((n,), a.time_delay_obs_act), torch.full((n,), a.normalize)))
+            else:
+                plist.append(ExecEnvParams(tid, torch.full((n,), a.task_size), torch.full((n,), a.reward_lambda),
+                                           torch.full((n,), a.time_delay_obs_act), torch.full((n,), a.normalize)))
+        return MultiAgentParams(loaded_params=loaded, agent_params=plist)
+
+    def action_space(self):
+        return self.action_spaces
+
+    def observation_space(self):
+        return self.observation_spaces
+
+    # -------------------------------------------------------------- plumbing
+    def _wrap(self, buf: torch.Tensor) -> MultiAgentState:
+        L = self.layout
+        agents, a = [], 0
+        for t, n in enumerate(self.multi_agent_config.number_of_agents_per_type):
+            agents.append(AgentStates(buf, L.agent_offsets[a:a + n], L.agent_kinds[a]))
+            a += n
+        return MultiAgentState(buf=buf, world_state=WorldState(buf, L), agent_states=agents)
+
+    def _outputs(self, E: int):
+        if self.persistent_outputs and self._out is not None and self._out["obs"].shape[0] == E:
+            return self._out
+        L, dev = self.layout, self.device
+        o = {"obs": torch.empty((E, self.num_agents, L.obs_stride), dtype=torch.float32, device=dev),
+             "rewards": torch.empty((E, self.num_agents), dtype=torch.float32, device=dev),
+             "done_all": torch.empty((E,), dtype=torch.int32, device=dev),
+             "dones": torch.empty((E, self.num_agents), dtype=torch.int32, device=dev),
+             "info": torch.empty((E, L.info_words), dtype=torch.int32, device=dev) if self.return_info else None}
+        o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
+                              _lib.ptr(o["dones"]), _lib.ptr(o["info"]) if o["info"] is not None else None)
+        if self.persistent_outputs:
+            self._out = o
+        return o
+
+    def _split_types(self, x: torch.Tensor, obs: bool):
+        out, a = [], 0
+        for n, d in zip(self.multi_agent_config.number_of_agents_per_type, self.layout.obs_dims):
+            out.append(x[:, a:a + n, :d] if obs else x[:, a:a + n])
+            a += n
+        return out
+
+    def _keys(self, key: torch.Tensor) -> torch.Tensor:
+        if key.dtype not in (torch.int32, torch.uint32) or key.dim() != 2 or key.shape[1] != 2:
+            raise ValueError("key must be a uint32/int32 tensor [E, 2] (one threefry key per env)")
+        return key.to(self.device).contiguous()
+
+    def _actions(self, actions, E: int) -> torch.Tensor:
+        if isinstance(actions, torch.Tensor):
+            a = actions
+        else:
+            cols = []
+            for x, n in zip(actions, self.multi_agent_config.number_of_agents_per_type):
+                x = torch.as_tensor(x, device=self.device)
+                cols.append(x.reshape(E, n))
+            a = torch.cat(cols, dim=1)
+        return a.to(device=self.device, dtype=torch.int32).reshape(E, self.num_agents).contiguous()
+
+    def _info(self, o, E):
+        if o["info"] is None:
+            return {}
+        info = o["info"]
+        f = info.view(torch.float32)
+
+        def col(k, isf):
+            return f[:, k] if isf else info[:, k]
+
+        world = {n: col(k, isf) for k, (n, isf) in enumerate(INFO_WORLD)}
+        world["time"] = torch.stack([world.pop("time_s"), world.pop("time_ns")], 1)
+        world["current_step"] = world["step_counter"]
+        agents, a = [], 0
+        for n_t in self.multi_agent_config.number_of_agents_per_type:
+            fields = INFO_MM if self.layout.agent_kinds[a] == AGENT_MM else INFO_EXE
+            d = {}
+            for k, (n, isf) in enumerate(fields):
+                idx = [INFO_WORLD_WORDS + (a + i) * INFO_AGENT_WORDS + k for i in range(n_t)]
+                d[n] = (f if isf else info)[:, idx]
+            agents.append(d)
+            a += n_t
+        return {"world": world, "agents": agents}
+
+    # ------------------------------------------------------------------ API
+    def reset(self, key: torch.Tensor, params: Optional[MultiAgentParams] = None):
+        """MARLEnv.reset / reset_env (marl_env.py:129-207, 763-770) for E envs."""
+        if params is None:
+            raise ValueError("Params must be provided to reset the environment.")
+        keys = self._keys(key)
+        E = keys.shape[0]
+        buf = torch.empty((E, self.layout.rec_words), dtype=torch.int32, device=self.device)
+        o = self._outputs(E)
+        _lib.check(_lib.lib().hftlob_env_reset(C.byref(self.cfg_c), E, _lib.ptr(keys),
+                                               _lib.ptr(params.loaded_params.message_data),
+                                               _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(buf),
+                                               C.byref(o["struct"]), _lib.stream_ptr()))
+        return self._split_types(o["obs"], True), self._wrap(buf)
+
+    reset_env = reset
+
+    def step(self, key: torch.Tensor, state: MultiAgentState, actions, params: MultiAgentParams,
+             reset_state=None):
+        """MARLEnv.step (marl_env.py:775-804) for E envs: step_env + auto-reset, one launch."""
+        if reset_state is not None:
+            raise NotImplementedError("Get obs on the MARL level is not implemented yet")  # as the reference
+        keys = self._keys(key)
+        E = keys.shape[0]
+        acts = self._actions(actions, E)
+        o = self._outputs(E)
+        _lib.check(_lib.lib().hftlob_env_step(C.byref(self.cfg_c), E, _lib.ptr(keys), _lib.ptr(acts),
+                                              _lib.ptr(params.loaded_params.message_data),
+                                              _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf),
+                                              C.byref(o["struct"]), _lib.stream_ptr()))
+        obs = self._split_types(o["obs"], True)
+        rewards = self._split_types(o["rewards"], False)
+        dones = {"__all__": o["done_all"].bool(), "agents": [d.bool() for d in self._split_types(o["dones"], False)]}
+        return obs, state, rewards, dones, self._info(o, E)
+
+    def sample_actions(self, key: torch.Tensor) -> torch.Tensor:
+        """Speed_test.py:166-177 random actions on device: int32 [E, num_agents]."""
+        keys = self._keys(key)
+        acts = torch.empty((keys.shape[0], self.num_agents), dtype=torch.int32, device=self.device)
+        _lib.check(_lib.lib().hftlob_sample_actions(C.byref(self.cfg_c), keys.shape[0], _lib.ptr(keys),
+                                                    _lib.ptr(acts), _lib.stream_ptr()))
+        return acts
+
+
+def split_keys(keys: torch.Tensor, n: int, partitionable: bool = True) -> torch.Tensor:
+    """jax.random.split per row: uint32 [E, 2] -> [E, n, 2] (device)."""
+    keys = keys.contiguous()
+    out = torch.empty((keys.shape[0], n, 2), dtype=keys.dtype, device=keys.device)
+    _lib.check(_lib.lib().hftlob_split_keys(keys.shape[0], n, int(partitionable), _lib.ptr(keys), _lib.ptr(out),
+                                            _lib.stream_ptr()))
+    return out

@@ -1,0 +1,142 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (ctypes binding of oracle/_build/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline import this.
+numpy in, numpy out; same C structs as include/hftlob.h (packed by
+hftlob.layout), so the oracle and the HIP path consume identical configs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        vp = C.c_void_p
+        L.oracle_book_process.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
+        L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+        L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
+        L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
+        L.oracle_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)] * 2
+        L.oracle_randint.argtypes = [vp, C.c_int32, C.c_int32, C.c_int]
+        L.oracle_randint.restype = C.c_int32
+        L.oracle_permutation.argtypes = [vp, C.c_int, C.c_int, vp]
+        L.oracle_abi_layout.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def _chk(rc):
+    if rc != 0:
+        raise RuntimeError(f"oracle error {rc}")
+
+
+def threefry2x32(k0, k1, x0, x1):
+    o0, o1 = C.c_uint32(), C.c_uint32()
+    lib().oracle_threefry2x32(k0, k1, x0, x1, C.byref(o0), C.byref(o1))
+    return o0.value, o1.value
+
+
+def randint(key, lo, hi, partitionable=True):
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    return int(lib().oracle_randint(_p(k), lo, hi, int(partitionable)))
+
+
+def permutation(key, n, partitionable=True):
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(n, dtype=np.int32)
+    lib().oracle_permutation(_p(k), n, int(partitionable), _p(out))
+    return out
+
+
+def split_keys(keys, n, partitionable=True):
+    keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
+    out = np.zeros((keys.shape[0], n, 2), dtype=np.uint32)
+    lib().oracle_split_keys(keys.shape[0], n, int(partitionable), _p(keys), _p(out))
+    return out
+
+
+def book_process(lob_cfg, msgs, asks, bids, trades, save_best=True):
+    """scan_through_entire_array[_save_bidask] over a batch; returns new arrays."""
+    msgs = np.ascontiguousarray(msgs, dtype=np.int32)
+    asks, bids, trades = (np.array(x, dtype=np.int32, copy=True, order="C") for x in (asks, bids, trades))
+    E, M = msgs.shape[0], msgs.shape[1]
+    ba = np.zeros((E, M, 2), dtype=np.int32) if save_best else None
+    bb = np.zeros((E, M, 2), dtype=np.int32) if save_best else None
+    _chk(lib().oracle_book_process(C.byref(lob_cfg), E, M, _p(msgs), _p(asks), _p(bids), _p(trades), _p(ba), _p(bb)))
+    return asks, bids, trades, ba, bb
+
+
+def env_reset(env_cfg, keys, init_states):
+    keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
+    E = keys.shape[0]
+    state = np.zeros((E, env_cfg.rec_words), dtype=np.int32)
+    obs = np.zeros((E, env_cfg.n_agents, env_cfg.obs_stride), dtype=np.float32)
+    init_states = np.ascontiguousarray(init_states, dtype=np.int32)
+    _chk(lib().oracle_env_reset(C.byref(env_cfg), E, _p(keys), _p(init_states), _p(state), _p(obs)))
+    return state, obs
+
+
+def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=True):
+    """Returns (state', obs, rewards, done_all, dones, info); `state` is not modified."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
+    E = keys.shape[0]
+    actions = np.ascontiguousarray(actions, dtype=np.int32).reshape(E, env_cfg.n_agents)
+    st = np.array(state, dtype=np.int32, copy=True, order="C")
+    obs = np.zeros((E, env_cfg.n_agents, env_cfg.obs_stride), dtype=np.float32)
+    rew = np.zeros((E, env_cfg.n_agents), dtype=np.float32)
+    da = np.zeros(E, dtype=np.int32)
+    dn = np.zeros((E, env_cfg.n_agents), dtype=np.int32)
+    info = np.zeros((E, env_cfg.info_words), dtype=np.int32) if with_info else None
+    _chk(lib().oracle_env_step(C.byref(env_cfg), E, _p(keys), _p(actions), _p(np.ascontiguousarray(msg_data, np.int32)),
+                               _p(np.ascontiguousarray(init_states, np.int32)), _p(st), _p(obs), _p(rew), _p(da),
+                               _p(dn), _p(info)))
+    return st, obs, rew, da, dn, info
+
+
+def sample_actions(env_cfg, keys):
+    keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
+    out = np.zeros((keys.shape[0], env_cfg.n_agents), dtype=np.int32)
+    lib().oracle_sample_actions(C.byref(env_cfg), keys.shape[0], _p(keys), _p(out))
+    return out
+
+
+def abi_layout():
+    out = np.zeros(8, dtype=np.int32)
+    lib().oracle_abi_layout(_p(out))
+    return out
+
+
+def init_states(env_cfg_lob, windows, msgs, world_cfg, init_rec_words):
+    """Init-state table via the oracle engine (BaseLOBEnv._init_states, CPU)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "jaxmarl-hft_amd"))
+    from hftlob.data.windows import init_messages, loaded_rows
+    W = len(windows.starts)
+    ft = msgs[windows.starts, 6:8].astype(np.int32)
+    im = init_messages(windows.books, ft, world_cfg.book_depth, world_cfg.init_id)
+    a0 = np.full((W, world_cfg.nOrders, 6), -1, np.int32)
+    t0 = np.full((W, world_cfg.nTrades, 8), -1, np.int32)
+    a, b, t, _, _ = book_process(env_cfg_lob, im, a0, a0, t0, save_best=False)
+    return loaded_rows(a, b, t, ft, windows, world_cfg.n_data_msg_per_step, init_rec_words)

@@ -1,0 +1,56 @@
+"""Seeded random message streams that exercise the engine's quirks (test helper)."""
+import numpy as np
+
+
+def random_streams(n_env, n_msg, seed, price0=1000, tick=1, spread=12, init_frac=0.1, garbage=0.02, nO=100):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.zeros((n_env, n_msg, 8), dtype=np.int32)
+    for e in range(n_env):
+        live = []                       # (oid, side, price)
+        next_oid = 1000
+        t, tn = 34200, 0
+        for k in range(n_msg):
+            if rng.random() < 0.8:
+                tn += int(rng.integers(1, 1000))
+            if rng.random() < 0.05:
+                t += 1
+            u = rng.random()
+            side = int(rng.choice([-1, 1]))
+            price = price0 + side * int(rng.integers(-3, spread)) * tick
+            qty = int(rng.integers(1, 60))
+            if rng.random() < 0.01:
+                qty = int(rng.integers(-3, 1))
+            tid = int(rng.integers(1, 6))
+            if u < 0.45:
+                typ, oid = 1, next_oid
+                next_oid += 1
+                live.append((oid, side, price))
+            elif u < 0.72:
+                typ = int(rng.choice([2, 3]))
+                if live and rng.random() < 0.75:
+                    oid, side, price = live[int(rng.integers(0, len(live)))]
+                elif rng.random() < init_frac * 5:
+                    oid = -2 - int(rng.integers(0, 3))      # init-id fallback path
+                else:
+                    oid = int(rng.integers(1, 5000))
+            elif u < 0.95:
+                typ = 4
+                oid = live[int(rng.integers(0, len(live)))][0] if live else 7
+            elif u < 1.0 - garbage:
+                typ, side, qty, price, oid = 0, 0, 0, 0, 0
+            else:
+                typ = int(rng.choice([0, 5, 6, 7])); side = int(rng.choice([-1, 0, 1])); oid = 9
+            out[e, k] = (typ, side, qty, price, oid, tid, t, tn)
+    return out
+
+
+def init_book_messages(n_env, seed, price0=1000, tick=1, depth=10):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    m = np.zeros((n_env, 2 * depth, 8), dtype=np.int32)
+    for e in range(n_env):
+        for k in range(2 * depth):
+            lvl = k // 2 + 1
+            side = -1 if k % 2 == 0 else 1
+            q = int(rng.integers(0, 200)) if rng.random() > 0.1 else 0
+            m[e, k] = (1, side, q, price0 - side * lvl * tick + (5 if side == -1 else -5), -2, -2 - k, 34199, 0)
+    return m
