@@ -1,0 +1,192 @@
+"""Throughput benchmark: env steps/sec of the 2-agent MARL LOB env (MM + EXE,
+2_player_fq_fqc.json), NUM_ENVS=4096 per GPU, Speed_test semantics
+(gymnax_exchange/jaxen/Speed_test.py:140-224):
+
+  per step:  rng, *step_keys = split(rng, NUM_ENVS + 1)
+             actions = per-type randint from split(step_key, n_types)   (device)
+             env.step(step_key, state, actions, params)                  (one fused HIP launch)
+
+Weak scaling: every rank (one process per GPU) steps its own 4096 envs on a
+replicated synthetic LOBSTER day; no collective on the data path (only the
+timing barrier / max-over-ranks).  Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "jaxmarl-hft_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+NUM_ENVS = 4096
+CONFIG = "2_player_fq_fqc"
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_env_step(env) -> int:
+    """HBM bytes one env-step must move, from the live layout."""
+    L, cfg = env.layout, env.multi_agent_config
+    nO, nT, M, D = L.n_orders, L.n_trades, L.n_msgs, L.n_data_msg
+    agent_words = sum(5 if k == 0 else 13 for k in L.agent_kinds)
+    n_ag = len(L.agent_kinds)
+    obs = sum(L.obs_dims[t] for t in L.agent_types)
+    reads = 32 * D + 2 * 24 * nO + 16 + 11 * 4 + 4 * agent_words + 4 * n_ag + 8
+    writes = 2 * 24 * nO + 32 * nT + 2 * 8 * M + 6 * 4 + 4 * agent_words + 4 * obs + 4 * n_ag + 4 * (1 + n_ag)
+    reset = (4 * L.init_rec_words + 2 * 8 * M + 4 * (5 + agent_words + obs)) // (cfg.world_config.episode_time)
+    return reads + writes + reset
+
+
+def cpu_baseline(env, day, n_envs, n_steps, threads):
+    """The CPU oracle (plain-C restatement of the reference, OpenMP over envs), timed on this host."""
+    sys.path.insert(0, ROOT)
+    from oracle import pyoracle as O
+    threads = O.set_threads(threads)
+    c = env.cfg_c
+    init = env._init_states.cpu().numpy()
+    rng = np.arange(2, dtype=np.uint32)
+    keys = O.split_keys(rng[None], n_envs + 1)[0][1:]
+    state, _ = O.env_reset(c, keys, init)
+    t0 = time.perf_counter()
+    master = np.array([0, 1], np.uint32)
+    for _ in range(n_steps):
+        ks = O.split_keys(master[None], n_envs + 1)[0]
+        master, step_keys = ks[0].copy(), ks[1:].copy()
+        acts = O.sample_actions(c, step_keys)
+        state, *_ = O.env_step(c, step_keys, acts, day.msgs, init, state, with_info=False)
+    dt = time.perf_counter() - t0
+    return n_envs * n_steps / dt, threads
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--envs", type=int, default=NUM_ENVS, help="envs per GPU")
+    ap.add_argument("--n-msgs", type=int, default=400_000, help="synthetic day length (messages)")
+    ap.add_argument("--mid", type=int, default=2_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from hftlob.config_io import builtin_config
+    from hftlob.data.synthetic import generate_day
+    from hftlob.env import MARLEnv, split_keys
+    from hftlob import _lib
+
+    cfg = builtin_config(CONFIG)
+    w = cfg.world_config
+    snap = w.n_data_msg_per_step * w.start_resolution
+    cache = f"/tmp/hftlob_day_{args.n_msgs}_{args.mid}_{snap}.npz"
+    if rank == 0 and not os.path.exists(cache):
+        d = generate_day(n_msgs=args.n_msgs, mid=args.mid, snap_every=snap)
+        np.savez(cache + ".tmp.npz", msgs=d.msgs, books=d.books, snap_idx=d.snap_idx, tick=d.tick_size)
+        os.replace(cache + ".tmp.npz", cache)
+    if dist is not None:
+        dist.barrier()
+    from hftlob.data.synthetic import LobsterDay
+    z = np.load(cache)
+    day = LobsterDay(msgs=z["msgs"], books=z["books"], snap_idx=z["snap_idx"], tick_size=int(z["tick"]))
+
+    E = args.envs
+    env = MARLEnv(None, cfg, data=day, device=f"cuda:{local}", return_info=False, persistent_outputs=True)
+    params = env.default_params
+    # global key split, then this rank's slice (reference pmap layout: contiguous env blocks)
+    master = torch.tensor([[0, 0]], dtype=torch.int32, device="cuda")
+    all_keys = split_keys(master, world * E + 1)[0]
+    keys0 = all_keys[1 + rank * E: 1 + (rank + 1) * E].contiguous()
+    _, state = env.reset(keys0, params)
+    rng = torch.tensor([[0, 1 + rank]], dtype=torch.int32, device="cuda")
+
+    def one_step(rng, ev=None):
+        ks = split_keys(rng, E + 1)[0]
+        rng, step_keys = ks[0:1].contiguous(), ks[1:].contiguous()
+        acts = env.sample_actions(step_keys)
+        if ev is not None:
+            ev[0].record()
+        env.step(step_keys, state, acts, params)
+        if ev is not None:
+            ev[1].record()
+        return rng
+
+    for _ in range(args.warmup):
+        rng = one_step(rng)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        rng = one_step(rng, events[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    value = world * E * args.steps / elapsed
+    per_env = algorithmic_bytes_per_env_step(env)
+    achieved = per_env * E / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        n_env_cpu, n_steps_cpu = 4096, 64       # one full episode (incl. auto-reset) of the metric workload
+        v, thr = cpu_baseline(env, day, n_env_cpu, n_steps_cpu, args.cpu_threads)
+        cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": thr, "kind": "port",
+               "sample": f"{n_env_cpu} envs x {n_steps_cpu} steps of the same config/day, C oracle (OpenMP)"}
+    line = {
+        "metric": "env steps/sec (whole node), 2-agent MARL, 10-level LOB, NUM_ENVS=4096",
+        "value": round(value, 1),
+        "unit": "env steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": f"synthetic LOBSTER day ({args.n_msgs} msgs, PCG64 seed 20260403, mid {args.mid})",
+        "config": {"workload": f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, 112 msgs/step, "
+                               f"auto-reset, Speed_test rollout semantics",
+                   "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
+                     "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1206,3 +1206,17 @@ void oracle_abi_layout(int* out) {
     out[6] = (int)offsetof(hftlob_env_cfg, info_words);
     out[7] = (int)offsetof(hftlob_agent_type_cfg, task);
 }
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+/* thread count of the OpenMP loops (CPU-baseline sizing); returns the value in effect */
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}

@@ -39,6 +39,8 @@ def lib():
         L.oracle_randint.restype = C.c_int32
         L.oracle_permutation.argtypes = [vp, C.c_int, C.c_int, vp]
         L.oracle_abi_layout.argtypes = [vp]
+        L.oracle_set_threads.argtypes = [C.c_int]
+        L.oracle_set_threads.restype = C.c_int
         _lib = L
     return _lib
 
@@ -120,6 +122,10 @@ def sample_actions(env_cfg, keys):
     out = np.zeros((keys.shape[0], env_cfg.n_agents), dtype=np.int32)
     lib().oracle_sample_actions(C.byref(env_cfg), keys.shape[0], _p(keys), _p(out))
     return out
+
+
+def set_threads(n: int) -> int:
+    return int(lib().oracle_set_threads(n))
 
 
 def abi_layout():
