@@ -312,29 +312,36 @@ template <bool BID, int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, 
 }
 
 // ------------------------------------------------------------ trade log
+// The trade log lives in LDS, structure-of-arrays [8 fields][64*S rows], so a
+// lane reads its rows' fields bank-conflict-free and appends (rare) touch one
+// row.  Keeping it out of VGPRs keeps the message loop at 4 waves/SIMD.
 template <int S>
 struct Trades {
-    i32 f[8][S];
+    i32* t;  // LDS base, 8 * 64 * S words
+    static constexpr int R = 64 * S;
+    DEV i32 get(int k, int r) const { return t[k * R + r * 64 + lane_id()]; }
+    DEV i32 at(int k, int row) const { return uni(t[k * R + row]); }
 };
 template <int S> DEV void trades_fill(Trades<S>& T, i32 v) {
+    const int l = lane_id();
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
-        for (int r = 0; r < S; ++r) T.f[k][r] = v;
+        for (int r = 0; r < S; ++r) T.t[k * Trades<S>::R + r * 64 + l] = v;
 }
 template <int S> DEV void load_trades(Trades<S>& T, const i32* g, const Valid<S>& V) {
     const int l = lane_id();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
+        int4 a = make_int4(-1, -1, -1, -1), b = a;
         if (V.v[r]) {
             const int4* row = reinterpret_cast<const int4*>(g + (r * 64 + l) * 8);
-            int4 a = row[0], b = row[1];
-            T.f[0][r] = a.x; T.f[1][r] = a.y; T.f[2][r] = a.z; T.f[3][r] = a.w;
-            T.f[4][r] = b.x; T.f[5][r] = b.y; T.f[6][r] = b.z; T.f[7][r] = b.w;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) T.f[k][r] = -1;
+            a = row[0];
+            b = row[1];
         }
+        const int o = r * 64 + l, R = Trades<S>::R;
+        T.t[0 * R + o] = a.x; T.t[1 * R + o] = a.y; T.t[2 * R + o] = a.z; T.t[3 * R + o] = a.w;
+        T.t[4 * R + o] = b.x; T.t[5 * R + o] = b.y; T.t[6 * R + o] = b.z; T.t[7 * R + o] = b.w;
     }
 }
 template <int S> DEV void store_trades(const Trades<S>& T, i32* g, const Valid<S>& V) {
@@ -342,11 +349,21 @@ template <int S> DEV void store_trades(const Trades<S>& T, i32* g, const Valid<S
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         if (V.v[r]) {
+            const int o = r * 64 + l, R = Trades<S>::R;
             int4* row = reinterpret_cast<int4*>(g + (r * 64 + l) * 8);
-            row[0] = make_int4(T.f[0][r], T.f[1][r], T.f[2][r], T.f[3][r]);
-            row[1] = make_int4(T.f[4][r], T.f[5][r], T.f[6][r], T.f[7][r]);
+            row[0] = make_int4(T.t[0 * R + o], T.t[1 * R + o], T.t[2 * R + o], T.t[3 * R + o]);
+            row[1] = make_int4(T.t[4 * R + o], T.t[5 * R + o], T.t[6 * R + o], T.t[7 * R + o]);
         }
     }
+}
+// write trade row e (uniform) — lanes 0..7 store one field each
+template <int S> DEV void trade_put(Trades<S>& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5, i32 f6,
+                                    i32 f7) {
+    const int l = lane_id();
+    i32 v = f0;
+    v = l == 1 ? f1 : v; v = l == 2 ? f2 : v; v = l == 3 ? f3 : v;
+    v = l == 4 ? f4 : v; v = l == 5 ? f5 : v; v = l == 6 ? f6 : v; v = l == 7 ? f7 : v;
+    if (l < 8) T.t[l * Trades<S>::R + e] = v;
 }
 
 // ------------------------------------------------------ message handlers
@@ -369,16 +386,9 @@ template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, c
     const i32 rem = wsub(qtm, qt);
     bool pr[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) pr[r] = B.vt.v[r] && B.tr.f[4][r] == -1;  // trade[:,OID=4] == -1
+    for (int r = 0; r < S; ++r) pr[r] = B.vt.v[r] && B.tr.get(4, r) == -1;  // trade[:,OID=4] == -1
     const int e = first_true(pr, B.c.nT - 1);
-    sset(B.tr.f[0], e, pt);
-    sset(B.tr.f[1], e, wmul(wsub(0, m.side), wsub(qt, newq)));
-    sset(B.tr.f[2], e, ot);
-    sset(B.tr.f[3], e, m.oid);
-    sset(B.tr.f[4], e, m.t);
-    sset(B.tr.f[5], e, m.tns);
-    sset(B.tr.f[6], e, tt);
-    sset(B.tr.f[7], e, m.tid);
+    trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
     sset(s.q, top, newq);
     rzn(s, top, B.vs);
     s.ok = false;
@@ -492,14 +502,16 @@ template <int S> DEV void refresh_best(Book<S>& B) {
 // ================================================= K1: book_process kernel
 // scan_through_entire_array[_save_bidask] — JaxOrderBookArrays.py:736-823
 template <int S>
-__global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
+__global__ __launch_bounds__(64, 4) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
                                                      i32* __restrict__ asks, i32* __restrict__ bids,
                                                      i32* __restrict__ trades, i32* __restrict__ best_asks,
                                                      i32* __restrict__ best_bids) {
     const int e = blockIdx.x;
     if (e >= n_env) return;
+    __shared__ i32 trade_lds[8 * 64 * S];
     const int l = lane_id();
     Book<S> B;
+    B.tr.t = trade_lds;
     B.c = lobcfg(cfg);
     B.vs.init(B.c.nO);
     B.vt.init(B.c.nT);
@@ -916,8 +928,8 @@ DEV void trade_view(const Book<S>& B, TradeView<S>& V, bool use_ovr, int ovr_idx
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         const bool o = use_ovr && (r * 64 + l == ovr_idx);
-        const i32 p = o ? ovr[0] : B.tr.f[0][r], q = o ? ovr[1] : B.tr.f[1][r];
-        const i32 s4 = o ? ovr[4] : B.tr.f[4][r], pt = o ? ovr[6] : B.tr.f[6][r], at = o ? ovr[7] : B.tr.f[7][r];
+        const i32 p = o ? ovr[0] : B.tr.get(0, r), q = o ? ovr[1] : B.tr.get(1, r);
+        const i32 s4 = o ? ovr[4] : B.tr.get(4, r), pt = o ? ovr[6] : B.tr.get(6, r), at = o ? ovr[7] : B.tr.get(7, r);
         const bool v = B.vt.v[r] && p >= 0;
         V.valid[r] = v;
         V.P[r] = v ? p : 0; V.Q[r] = v ? q : 0; V.S4[r] = v ? s4 : 0; V.PT[r] = v ? pt : 0; V.AT[r] = v ? at : 0;
@@ -929,7 +941,7 @@ template <int S> DEV int first_any_neg1_trade(const Book<S>& B) {
     for (int r = 0; r < S; ++r) {
         bool any = false;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) any |= B.tr.f[k][r] == -1;
+        for (int k = 0; k < 8; ++k) any |= B.tr.get(k, r) == -1;
         pr[r] = B.vt.v[r] && any;
     }
     return first_true(pr, B.c.nT - 1);
@@ -1187,8 +1199,10 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 // ====================================================== K2: fused env step
 // MARLEnv.step — marl_env.py:775-804 (step_env :211-709, auto-reset select)
 #define MAX_AGENT_ROWS 128
-template <int S>
-__global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
+// NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
+// 100/100 default), which folds the slot-validity masks away.
+template <int S, int NFIX>
+__global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
                                                  const i32* __restrict__ actions, const i32* __restrict__ msg_data,
                                                  const i32* __restrict__ init_states, i32* __restrict__ state,
                                                  float* __restrict__ obs_out, float* __restrict__ rew_out,
@@ -1196,6 +1210,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                                                  i32* __restrict__ info_out) {
     __shared__ __attribute__((aligned(16))) i32 rows[MAX_AGENT_ROWS * 8];
     __shared__ i32 axs[HFTLOB_MAX_AGENTS * 6];  // per-agent action extras
+    __shared__ i32 trade_lds[8 * 64 * S];
     const int e = blockIdx.x;
     if (e >= n_env) return;
     const int l = lane_id();
@@ -1203,7 +1218,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
     i32* rec = state + (size_t)e * c.rec_words;
     Book<S> B;
+    B.tr.t = trade_lds;
     B.c = lobcfg(c.lob);
+    if (NFIX > 0) { B.c.nO = NFIX; B.c.nT = NFIX; }
     B.vs.init(B.c.nO);
     B.vt.init(B.c.nT);
     const Key key{keys[2 * e], keys[2 * e + 1]};
@@ -1369,6 +1386,11 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     WorldView wv;
     wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
     wv.vol_a = side_volume(B.a, B.vs); wv.vol_b = side_volume(B.b, B.vs);
+    // the book is final: store it now (frees its registers for the rewards);
+    // an auto-reset below overwrites the record anyway
+    store_side(B.a, rec + c.off_asks, B.vs);
+    store_side(B.b, rec + c.off_bids, B.vs);
+    store_trades(B.tr, rec + c.off_trades, B.vt);
     wv.step = wadd(step, 1); wv.max_steps = max_steps; wv.mid = X.last_mid;
     i32* info = info_out ? info_out + (size_t)e * c.info_words : nullptr;
     {
@@ -1457,9 +1479,6 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt);
         return;
     }
-    store_side(B.a, rec + c.off_asks, B.vs);
-    store_side(B.b, rec + c.off_bids, B.vs);
-    store_trades(B.tr, rec + c.off_trades, B.vt);
     if (l == 0) {
         rec[c.off_loaded + LD_STEP] = wadd(step, 1);
         i32* W = rec + c.off_world;
@@ -1592,11 +1611,13 @@ int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, 
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
-#define LAUNCH_STEP(SS) hipLaunchKernelGGL(k_env_step<SS>, g, b, 0, st, *cfg, n_env, keys, actions, msg_data, init_states, \
-                                           state, out->obs, out->rewards, out->done_all, out->dones, out->info)
-    if (S == 1) LAUNCH_STEP(1);
-    else if (S == 2) LAUNCH_STEP(2);
-    else LAUNCH_STEP(4);
+#define LAUNCH_STEP(SS, NF) hipLaunchKernelGGL((k_env_step<SS, NF>), g, b, 0, st, *cfg, n_env, keys, actions, msg_data, \
+                                               init_states, state, out->obs, out->rewards, out->done_all, out->dones, \
+                                               out->info)
+    if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100);
+    else if (S == 1) LAUNCH_STEP(1, 0);
+    else if (S == 2) LAUNCH_STEP(2, 0);
+    else LAUNCH_STEP(4, 0);
 #undef LAUNCH_STEP
     return launch_status();
 }
