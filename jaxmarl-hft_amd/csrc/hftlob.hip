@@ -100,6 +100,14 @@ DEV float wave_fsum(float v) {
 }
 DEV unsigned long long ballot(bool p) { return __ballot(p); }
 
+// Diagnostic build only (-DHFTLOB_STAMPS): per-phase shader-clock stamps of
+// k_env_step, written to the info buffer in place of the info fields.
+#ifdef HFTLOB_STAMPS
+#define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#else
+#define STAMP(var)
+#endif
+
 // ------------------------------------------------------------------ PRNG
 DEV u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
 DEV void threefry(u32 k0, u32 k1, u32 x0, u32 x1, u32& o0, u32& o1) {
@@ -158,6 +166,10 @@ DEV i32 randint(Key k, i32 lo, i32 hi, bool part) {
 }
 
 // --------------------------------------------------------- book side state
+// Style rule for the hot path: lane predicates are built as 64-bit lane masks
+// (v_cmp -> SGPR pair, combined with s_and/s_or), never as per-lane bool
+// arrays or short-circuit && (which hipcc lowers to exec-masked branches),
+// and single slots are read / written with v_readlane / v_writelane.
 struct LobCfg {
     i32 maxint, init_id, depth, cancel_mode, t4, check_fill, nO, nT;
 };
@@ -168,49 +180,75 @@ DEV LobCfg lobcfg(const hftlob_lob_cfg& c) {
     return o;
 }
 
+typedef unsigned long long lmask;
+DEV lmask bal(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+DEV int ffs64(lmask m) { return m ? (int)__builtin_ctzll(m) : -1; }
+
+// v_writelane_b32 through the LLVM intrinsic (compiler-managed hazards)
+extern "C" __device__ i32 __hftlob_writelane(i32 val, i32 lane, i32 old) __asm("llvm.amdgcn.writelane.i32");
+DEV i32 wlane(i32 old, i32 val, int l) { return __hftlob_writelane(val, l, old); }
+
 template <int S>
 struct Side {
     i32 p[S], q[S], oid[S], tid[S], ts[S], tns[S];
-    i32 best_p, best_q;  // cached (price, volume) of get_best_*; valid when ok
+    // wave-uniform bookkeeping (SGPRs)
+    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid when ok
     bool ok;             // cache valid
-    bool clean;          // every slot with q <= 0 is an all -1 row (see rzn)
+    bool clean;          // every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
+                         // ever has to look at the row just written
+    bool neg1;           // some row with p != -1 holds a -1 in another field (then "first row
+                         // holding ANY -1" needs the full test, else p == -1 suffices)
 };
 
-// uniform-index slot access
-template <int S> DEV i32 sget(const i32 (&a)[S], int idx) {
-    const int r = idx >> 6, l = idx & 63;
-    i32 v = rdl(a[0], l);
-#pragma unroll
-    for (int k = 1; k < S; ++k) if (r == k) v = rdl(a[k], l);
-    return v;
-}
-template <int S> DEV void sset(i32 (&a)[S], int idx, i32 val) {
-    const int r = idx >> 6, l = idx & 63;
-#pragma unroll
-    for (int k = 0; k < S; ++k) if (r == k) a[k] = wrl(a[k], val, l);
-}
-template <int S> DEV void clear_slot(Side<S>& s, int idx) {
-    sset(s.p, idx, -1); sset(s.q, idx, -1); sset(s.oid, idx, -1);
-    sset(s.tid, idx, -1); sset(s.ts, idx, -1); sset(s.tns, idx, -1);
-}
-template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
-#pragma unroll
-    for (int r = 0; r < S; ++r) {
-        unsigned long long b = ballot(pr[r]);
-        if (b) return r * 64 + (int)__builtin_ctzll(b);
-    }
-    return fallback;
-}
-
 template <int S>
-struct Valid {
+struct Valid {  // slot (or trade row) r*64+lane exists
+    lmask m[S];
     bool v[S];
     DEV void init(int n) {
         const int l = lane_id();
 #pragma unroll
-        for (int r = 0; r < S; ++r) v[r] = r * 64 + l < n;
+        for (int r = 0; r < S; ++r) {
+            v[r] = r * 64 + l < n;
+            const int k = n - r * 64;
+            m[r] = k >= 64 ? ~0ull : (k <= 0 ? 0ull : ((1ull << k) - 1ull));
+        }
     }
 };
+
+// run BODY for the register set holding uniform slot e
+#define ON_SLOT(S_, e_, BODY)                                       \
+    {                                                               \
+        const int r_ = (e_) >> 6, l_ = (e_)&63;                     \
+        _Pragma("unroll") for (int k_ = 0; k_ < (S_); ++k_) {       \
+            if ((S_) == 1 || r_ == k_) { BODY }                     \
+        }                                                           \
+    }
+
+template <int S> DEV i32 sget(const i32 (&a)[S], int e) {
+    i32 v = 0;
+    ON_SLOT(S, e, v = rdl(a[k_], l_);)
+    return v;
+}
+template <int S> DEV void sset(i32 (&a)[S], int e, i32 val) { ON_SLOT(S, e, a[k_] = wlane(a[k_], val, l_);) }
+template <int S> DEV void put_row(Side<S>& s, int e, i32 p, i32 q, i32 oid, i32 tid, i32 ts, i32 tns) {
+    ON_SLOT(S, e, s.p[k_] = wlane(s.p[k_], p, l_); s.q[k_] = wlane(s.q[k_], q, l_);
+            s.oid[k_] = wlane(s.oid[k_], oid, l_); s.tid[k_] = wlane(s.tid[k_], tid, l_);
+            s.ts[k_] = wlane(s.ts[k_], ts, l_); s.tns[k_] = wlane(s.tns[k_], tns, l_);)
+}
+template <int S> DEV void clear_slot(Side<S>& s, int e) { put_row(s, e, -1, -1, -1, -1, -1, -1); }
+// first slot over per-register lane masks; `fallback` if none
+template <int S> DEV int first_slot(const lmask (&m)[S], int fallback) {
+    int idx = fallback;
+#pragma unroll
+    for (int r = S - 1; r >= 0; --r) idx = m[r] ? r * 64 + ffs64(m[r]) : idx;
+    return idx;
+}
+template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
+    lmask m[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) m[r] = bal(pr[r]);
+    return first_slot(m, fallback);
+}
 
 template <int S> DEV void load_side(Side<S>& s, const i32* g, const Valid<S>& V) {
     const int l = lane_id();
@@ -225,13 +263,18 @@ template <int S> DEV void load_side(Side<S>& s, const i32* g, const Valid<S>& V)
             s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
         }
     }
-    // clean: every slot with q <= 0 is all -1 (then targeted removal == _removeZeroNegQuant)
-    bool bad = false;
+    lmask bad = 0, n1 = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r)
-        bad |= V.v[r] && s.q[r] <= 0 &&
-               !(s.p[r] == -1 && s.q[r] == -1 && s.oid[r] == -1 && s.tid[r] == -1 && s.ts[r] == -1 && s.tns[r] == -1);
-    s.clean = ballot(bad) == 0ull;
+    for (int r = 0; r < S; ++r) {
+        const lmask any = bal(s.p[r] == -1) | bal(s.q[r] == -1) | bal(s.oid[r] == -1) | bal(s.tid[r] == -1) |
+                          bal(s.ts[r] == -1) | bal(s.tns[r] == -1);
+        const lmask all = bal(s.p[r] == -1) & bal(s.q[r] == -1) & bal(s.oid[r] == -1) & bal(s.tid[r] == -1) &
+                          bal(s.ts[r] == -1) & bal(s.tns[r] == -1);
+        bad |= V.m[r] & bal(s.q[r] <= 0) & ~all;
+        n1 |= V.m[r] & ~bal(s.p[r] == -1) & any;
+    }
+    s.clean = bad == 0ull;
+    s.neg1 = n1 != 0ull;
     s.ok = false;
 }
 template <int S> DEV void store_side(const Side<S>& s, i32* g, const Valid<S>& V) {
@@ -247,11 +290,11 @@ template <int S> DEV void store_side(const Side<S>& s, i32* g, const Valid<S>& V
     }
 }
 
-// _removeZeroNegQuant — JaxOrderBookArrays.py:85-90.  Full pass over the side
-// when the side may hold stray q<=0 rows, else only the slot just written.
-template <int S> DEV void rzn(Side<S>& s, int idx, const Valid<S>& V) {
+// _removeZeroNegQuant — JaxOrderBookArrays.py:85-90, after row e was written
+// with quantity qe.  Clean side: only row e can hold q <= 0.
+template <int S> DEV void rzn(Side<S>& s, int e, i32 qe) {
     if (s.clean) {
-        if (sget(s.q, idx) <= 0) clear_slot(s, idx);
+        if (qe <= 0) clear_slot(s, e);
     } else {
 #pragma unroll
         for (int r = 0; r < S; ++r)
@@ -269,7 +312,7 @@ template <int S> DEV void best_bid(Side<S>& s, const Valid<S>& V) {
     const i32 mp = wave_max(m);
     i32 v = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.p[r] == mp) ? s.q[r] : 0);
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] & (s.p[r] == mp)) ? s.q[r] : 0);
     s.best_p = mp;
     s.best_q = wave_sum(v);
     s.ok = true;
@@ -283,13 +326,14 @@ template <int S> DEV void best_ask(Side<S>& s, const Valid<S>& V, i32 maxint) {
     const i32 pa = mn == maxint ? -1 : mn;
     i32 v = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.p[r] == pa) ? s.q[r] : 0);
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] & (s.p[r] == pa)) ? s.q[r] : 0);
     s.best_p = pa;
     s.best_q = wave_sum(v);
     s.ok = true;
 }
 
-// _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas)
+// _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
+// mp is the side's max price (bid) / min price with -1 -> maxint (ask)
 template <bool BID, int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, const LobCfg& c, i32 mp) {
     i32 t[S], n[S], m = INT_MAX;
 #pragma unroll
@@ -305,10 +349,10 @@ template <bool BID, int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, 
         m = imin_(m, V.v[r] ? n[r] : INT_MAX);
     }
     const i32 mtn = wave_min(m);
-    bool pr[S];
+    lmask pm[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) pr[r] = V.v[r] && n[r] == mtn;
-    return first_true(pr, c.nO - 1);
+    for (int r = 0; r < S; ++r) pm[r] = V.m[r] & bal(n[r] == mtn);
+    return first_slot(pm, c.nO - 1);
 }
 
 // ------------------------------------------------------------ trade log
@@ -379,25 +423,57 @@ struct Msg {
     i32 type, side, price, qty, oid, tid, t, tns;
 };
 
+// Incremental best-quote bookkeeping.  Every update below is exact for a clean
+// side: it changes (best_p, best_q) only where get_best_* / get_volume_at_price
+// would, and falls back to a full recompute (ok = false) where it cannot tell.
+template <bool BID, int S> DEV void note_add(Side<S>& s, i32 np, i32 nq, i32 maxint) {
+    // an all -1 row now holds (np, nq > 0)
+    if (!s.ok) return;
+    if (BID) {
+        if (s.best_p == -1) {
+            if (np > -1) { s.best_p = np; s.best_q = nq; } else s.ok = false;
+        } else if (np > s.best_p) { s.best_p = np; s.best_q = nq; }
+        else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
+    } else {
+        if (np == -1 || np == maxint) { if (s.best_p == -1) s.ok = false; return; }
+        if (s.best_p == -1 || np < s.best_p) { s.best_p = np; s.best_q = nq; }
+        else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
+    }
+}
+// a row at price op lost dq of its quantity (possibly all of it)
+template <int S> DEV void note_reduce(Side<S>& s, i32 op, i32 dq) {
+    if (!s.ok) return;
+    if (op == -1 || s.best_p == -1) { s.ok = false; return; }
+    if (op != s.best_p) return;
+    s.best_q = wsub(s.best_q, dq);
+    if (s.best_q <= 0) s.ok = false;  // level exhausted (or odd data): rescan
+}
+
 // match_order — JaxOrderBookArrays.py:172-220
 template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
-    const i32 qt = sget(s.q, top), pt = sget(s.p, top), ot = sget(s.oid, top), tt = sget(s.tid, top);
+    i32 qt = 0, pt = 0, ot = 0, tt = 0;
+    ON_SLOT(S, top, qt = rdl(s.q[k_], l_); pt = rdl(s.p[k_], l_); ot = rdl(s.oid[k_], l_); tt = rdl(s.tid[k_], l_);)
     const i32 newq = imax_(0, wsub(qt, qtm));
     const i32 rem = wsub(qtm, qt);
-    bool pr[S];
+    lmask fm[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) pr[r] = B.vt.v[r] && B.tr.get(4, r) == -1;  // trade[:,OID=4] == -1
-    const int e = first_true(pr, B.c.nT - 1);
+    for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(B.tr.get(4, r) == -1);  // trade[:,OID=4] == -1
+    const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
-    sset(s.q, top, newq);
-    rzn(s, top, B.vs);
-    s.ok = false;
+    if (s.clean) {
+        if (newq <= 0) clear_slot(s, top);
+        else sset(s.q, top, newq);
+        note_reduce(s, pt, wsub(qt, newq));
+    } else {
+        sset(s.q, top, newq);
+        rzn(s, top, newq);
+    }
     return rem;
 }
 
-// _match_against_{bid,ask}_orders — :284-331.  `mp` shortcut: the top slot's
-// price never beats the side's best, so "best does not cross" ends the loop
-// exactly; only a crossing best pays for the full 3-reduction top-of-book.
+// _match_against_{bid,ask}_orders — :284-331.  The top slot's price never
+// beats the side's best, so "best does not cross" ends the loop exactly; only
+// a crossing best pays for the 3-reduction top-of-book.
 template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     while (qtm > 0) {
         if (!s.ok) { if (BID) best_bid(s, B.vs); else best_ask(s, B.vs, B.c.maxint); }
@@ -412,29 +488,49 @@ template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm
 }
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
-template <int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
-    bool pr[S];
+template <bool BID, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
+    lmask fm[S];
+    const bool fast = s.clean && !s.neg1;  // then "any -1" <=> p == -1
+    if (fast) {
 #pragma unroll
-    for (int r = 0; r < S; ++r)
-        pr[r] = B.vs.v[r] && (s.p[r] == -1 || s.q[r] == -1 || s.oid[r] == -1 || s.tid[r] == -1 ||
-                              s.ts[r] == -1 || s.tns[r] == -1);
-    const int e = first_true(pr, B.c.nO - 1);
-    sset(s.p, e, m.price); sset(s.q, e, imax_(0, qty)); sset(s.oid, e, m.oid);
-    sset(s.tid, e, m.tid); sset(s.ts, e, m.t);          sset(s.tns, e, m.tns);
-    rzn(s, e, B.vs);
-    s.ok = false;
+        for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(s.p[r] == -1);
+    } else {
+#pragma unroll
+        for (int r = 0; r < S; ++r)
+            fm[r] = B.vs.m[r] & (bal(s.p[r] == -1) | bal(s.q[r] == -1) | bal(s.oid[r] == -1) |
+                                 bal(s.tid[r] == -1) | bal(s.ts[r] == -1) | bal(s.tns[r] == -1));
+    }
+    const int e = first_slot(fm, B.c.nO - 1);
+    const i32 nq = imax_(0, qty);
+    if (!s.clean) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
+        put_row(s, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        rzn(s, e, nq);
+        return;
+    }
+    i32 op = 0, oq = 0;
+    ON_SLOT(S, e, op = rdl(s.p[k_], l_); oq = rdl(s.q[k_], l_);)
+    const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
+    if (nq > 0) {
+        put_row(s, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1))) s.neg1 = true;
+        if (was_empty) note_add<BID>(s, m.price, nq, B.c.maxint);
+        else s.ok = false;
+    } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
+        clear_slot(s, e);
+        s.ok = false;
+    }
 }
 
 // check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max)
 template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
-    bool neg = false;
+    lmask neg = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(s.p[r] < 0);
+    if (neg != 0ull) return;
     i32 w = BID ? INT_MAX : INT_MIN;
 #pragma unroll
-    for (int r = 0; r < S; ++r) {
-        neg |= B.vs.v[r] && s.p[r] < 0;
+    for (int r = 0; r < S; ++r)
         w = BID ? imin_(w, B.vs.v[r] ? s.p[r] : INT_MAX) : imax_(w, B.vs.v[r] ? s.p[r] : INT_MIN);
-    }
-    if (ballot(neg) != 0ull) return;
     const i32 worst = BID ? wave_min(w) : wave_max(w);
 #pragma unroll
     for (int r = 0; r < S; ++r)
@@ -448,7 +544,7 @@ template <int S> DEV void bid_lim(Book<S>& B, Msg m) {
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
     if (B.c.check_fill) evict_if_full<true>(B, B.b);
     const bool discard = (B.c.t4 == 0 || B.c.t4 == 2) && m.type == 4;
-    if (!discard) add_order(B, B.b, m, rem);
+    if (!discard) add_order<true>(B, B.b, m, rem);
 }
 // ask_lim — :446-508
 template <int S> DEV void ask_lim(Book<S>& B, Msg m) {
@@ -456,43 +552,48 @@ template <int S> DEV void ask_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<true>(B, B.b, m.qty, m.price, m);
     if (B.c.check_fill) evict_if_full<false>(B, B.a);
     const bool discard = (B.c.t4 == 0 || B.c.t4 == 2) && m.type == 4;
-    if (!discard) add_order(B, B.a, m, rem);
+    if (!discard) add_order<false>(B, B.a, m, rem);
 }
 // cancel_order + get_init_id_match — :93-139
 template <int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
-    bool pr[S];
+    lmask fm[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) pr[r] = B.vs.v[r] && s.oid[r] == m.oid;
-    int idx = first_true(pr, -1);
+    for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(s.oid[r] == m.oid);
+    int idx = first_slot(fm, -1);
     if (idx < 0) {
         const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
 #pragma unroll
         for (int r = 0; r < S; ++r)
-            pr[r] = B.vs.v[r] && s.p[r] == m.price && s.oid[r] <= B.c.init_id && s.oid[r] >= lo && s.q[r] >= m.qty;
-        idx = first_true(pr, B.c.nO - 1);  // -1 wraps to the last slot
+            fm[r] = B.vs.m[r] & bal(s.p[r] == m.price) & bal(s.oid[r] <= B.c.init_id) & bal(s.oid[r] >= lo) &
+                    bal(s.q[r] >= m.qty);
+        idx = first_slot(fm, B.c.nO - 1);  // -1 wraps to the last slot
     }
-    const i32 old_p = sget(s.p, idx);
-    sset(s.q, idx, wsub(sget(s.q, idx), m.qty));
-    const bool was_clean = s.clean;
-    rzn(s, idx, B.vs);
-    // best quote unchanged iff the touched slot was neither at the best price
-    // nor empty and the side was not empty (price/volume sets then unchanged)
-    if (!(was_clean && s.ok && old_p != s.best_p && old_p != -1 && s.best_p != -1)) s.ok = false;
+    i32 op = 0, oq = 0;
+    ON_SLOT(S, idx, op = rdl(s.p[k_], l_); oq = rdl(s.q[k_], l_);)
+    const i32 nq = wsub(oq, m.qty);
+    if (s.clean) {
+        if (nq <= 0) clear_slot(s, idx);
+        else sset(s.q, idx, nq);
+        note_reduce(s, op, wsub(oq, nq > 0 ? nq : 0));
+    } else {
+        sset(s.q, idx, nq);
+        rzn(s, idx, nq);
+    }
 }
 
-// cond_type_side_save_bidask — :687-732 (dispatch index exactly as reference)
+// cond_type_side_save_bidask — :687-732: dispatch index
+//   1 side==1 & type in {1,4}; 2 side==-1 & type in {2,3}; 3 side==1 & type in {2,3};
+//   4 side==0 & type==0 (doNothing); everything else 0 (ask_lim); side flipped for type 4
 template <int S> DEV void process_msg(Book<S>& B, i32 d0, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
     m.type = d0;
     m.side = d0 == 4 ? wsub(0, d1) : d1;
     m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
-    const bool lim = (m.type == 1) || (m.type == 4), cnl = (m.type == 2) || (m.type == 3);
-    const int index = (m.side == 1 && lim) * 1 + (m.side == -1 && cnl) * 2 + (m.side == 1 && cnl) * 3 +
-                      (m.side == 0 && m.type == 0) * 4;
-    if (index == 0) ask_lim(B, m);
-    else if (index == 1) bid_lim(B, m);
-    else if (index == 2) cancel(B, B.a, m);
-    else if (index == 3) cancel(B, B.b, m);
+    const bool cnl = (d0 == 2) | (d0 == 3);
+    if (cnl & (m.side == -1)) cancel(B, B.a, m);
+    else if (cnl & (m.side == 1)) cancel(B, B.b, m);
+    else if (((d0 == 1) | (d0 == 4)) & (m.side == 1)) bid_lim(B, m);
+    else if (!((d0 == 0) & (m.side == 0))) ask_lim(B, m);
 }
 template <int S> DEV void refresh_best(Book<S>& B) {
     if (!B.a.ok) best_ask(B.a, B.vs, B.c.maxint);
@@ -502,7 +603,7 @@ template <int S> DEV void refresh_best(Book<S>& B) {
 // ================================================= K1: book_process kernel
 // scan_through_entire_array[_save_bidask] — JaxOrderBookArrays.py:736-823
 template <int S>
-__global__ __launch_bounds__(64, 4) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
+__global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
                                                      i32* __restrict__ asks, i32* __restrict__ bids,
                                                      i32* __restrict__ trades, i32* __restrict__ best_asks,
                                                      i32* __restrict__ best_bids) {
@@ -755,7 +856,7 @@ DEV void cancel_rows(const Side<S>& s, const Valid<S>& V, i32 agent, int size, i
     int n = 0;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        unsigned long long bm = ballot(V.v[r] && s.tid[r] == agent);
+        unsigned long long bm = V.m[r] & bal(s.tid[r] == agent);
         while (bm && n < size) {
             const int l = (int)__builtin_ctzll(bm);
             bm &= bm - 1;
@@ -1202,7 +1303,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
 template <int S, int NFIX>
-__global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
+__global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
                                                  const i32* __restrict__ actions, const i32* __restrict__ msg_data,
                                                  const i32* __restrict__ init_states, i32* __restrict__ state,
                                                  float* __restrict__ obs_out, float* __restrict__ rew_out,
@@ -1213,6 +1314,7 @@ __global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env,
     __shared__ i32 trade_lds[8 * 64 * S];
     const int e = blockIdx.x;
     if (e >= n_env) return;
+    STAMP(t_start);
     const int l = lane_id();
     const bool part = c.prng_partitionable;
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
@@ -1317,6 +1419,7 @@ __global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env,
         __syncthreads();
     }
 
+    STAMP(t_agents);
     // ---- (B)+(D) stream the combined messages through the book, 64 per chunk
     trades_fill(B.tr, -1);
     i32 dstart = wadd(start_index, wmul(D, step));
@@ -1382,6 +1485,7 @@ __global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env,
     X.ep_done = wsub(wsub(max_steps, step), 1) <= 1;
     const bool all = X.ep_done;
 
+    STAMP(t_book);
     // ---- (E) rewards, (G) agent states, (K) observations
     WorldView wv;
     wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
@@ -1462,6 +1566,7 @@ __global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env,
             }
         }
     }
+    STAMP(t_rewards);
     // ---- (F) world state + info
     const float new_mid = X.last_mid;
     const float dt = i2f(last_t0) + i2f(last_t1) / 1e9f - i2f(wt0) - i2f(wt1) / 1e9f;
@@ -1475,6 +1580,13 @@ __global__ __launch_bounds__(64, 4) void k_env_step(hftlob_env_cfg c, int n_env,
         if (l < HFTLOB_INFO_WORLD_WORDS) info[l] = v;
     }
     if (l == 0) done_all_out[e] = all;
+#ifdef HFTLOB_STAMPS
+    if (info && l == 0) {
+        const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+        info[0] = (i32)(t_agents - t_start); info[1] = (i32)(t_book - t_agents);
+        info[2] = (i32)(t_rewards - t_book); info[3] = (i32)(t_end - t_rewards); info[4] = (i32)all;
+    }
+#endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
         env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt);
         return;

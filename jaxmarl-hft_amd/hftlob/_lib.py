@@ -11,7 +11,7 @@ import os
 
 from .layout import EnvCfg, LobCfg, StepOut
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
+LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
 ABI_VERSION = 1
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
            "hftlob_env_step", "hftlob_sample_actions", "hftlob_split_keys")
