@@ -165,11 +165,19 @@ DEV i32 randint(Key k, i32 lo, i32 hi, bool part) {
     return (i32)((u32)lo + off);
 }
 
-// --------------------------------------------------------- book side state
+// ------------------------------------------------------------ book tables
+// Every table of the book (ask side, bid side, trade log) lives in LDS as
+// structure-of-arrays: field f of slot s at base[f * R + s], R = the table's
+// slot count.  A lane reads slots lane and lane+64 of one field with a
+// conflict-free column load; one slot is read with a broadcast load and
+// written by lanes 0..5 (one field each).  Keeping the book out of VGPRs
+// removes the whole-book register copies the compiler emits at the control
+// flow merges of the message dispatch, and LDS (8.4 KB per env for 100/100
+// slots) keeps all 16 envs of a CU resident.
+//
 // Style rule for the hot path: lane predicates are built as 64-bit lane masks
 // (v_cmp -> SGPR pair, combined with s_and/s_or), never as per-lane bool
-// arrays or short-circuit && (which hipcc lowers to exec-masked branches),
-// and single slots are read / written with v_readlane / v_writelane.
+// arrays or short-circuit && (which hipcc lowers to exec-masked branches).
 struct LobCfg {
     i32 maxint, init_id, depth, cancel_mode, t4, check_fill, nO, nT;
 };
@@ -188,17 +196,12 @@ DEV int ffs64(lmask m) { return m ? (int)__builtin_ctzll(m) : -1; }
 extern "C" __device__ i32 __hftlob_writelane(i32 val, i32 lane, i32 old) __asm("llvm.amdgcn.writelane.i32");
 DEV i32 wlane(i32 old, i32 val, int l) { return __hftlob_writelane(val, l, old); }
 
-template <int S>
-struct Side {
-    i32 p[S], q[S], oid[S], tid[S], ts[S], tns[S];
-    // wave-uniform bookkeeping (SGPRs)
-    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid when ok
-    bool ok;             // cache valid
-    bool clean;          // every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
-                         // ever has to look at the row just written
-    bool neg1;           // some row with p != -1 holds a -1 in another field (then "first row
-                         // holding ANY -1" needs the full test, else p == -1 suffices)
-};
+// Lanes of one wave exchange data through LDS without a barrier (a wave's LDS
+// operations complete in order); this only stops the compiler from moving a
+// load across a store another lane made.
+DEV void lds_order() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+
+enum { FP = 0, FQ, FOID, FTID, FTS, FTNS };  // order-side fields (JaxOrderBookArrays.py:21-28)
 
 template <int S>
 struct Valid {  // slot (or trade row) r*64+lane exists
@@ -215,27 +218,29 @@ struct Valid {  // slot (or trade row) r*64+lane exists
     }
 };
 
-// run BODY for the register set holding uniform slot e
-#define ON_SLOT(S_, e_, BODY)                                       \
-    {                                                               \
-        const int r_ = (e_) >> 6, l_ = (e_)&63;                     \
-        _Pragma("unroll") for (int k_ = 0; k_ < (S_); ++k_) {       \
-            if ((S_) == 1 || r_ == k_) { BODY }                     \
-        }                                                           \
-    }
-
-template <int S> DEV i32 sget(const i32 (&a)[S], int e) {
-    i32 v = 0;
-    ON_SLOT(S, e, v = rdl(a[k_], l_);)
-    return v;
+// column load: o[r] = field f of slot r*64+lane (slots >= R read padding; mask with Valid)
+template <int S> DEV void ldcol(const i32* t, int R, int f, i32 (&o)[S]) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) o[r] = t[f * R + r * 64 + l];
 }
-template <int S> DEV void sset(i32 (&a)[S], int e, i32 val) { ON_SLOT(S, e, a[k_] = wlane(a[k_], val, l_);) }
-template <int S> DEV void put_row(Side<S>& s, int e, i32 p, i32 q, i32 oid, i32 tid, i32 ts, i32 tns) {
-    ON_SLOT(S, e, s.p[k_] = wlane(s.p[k_], p, l_); s.q[k_] = wlane(s.q[k_], q, l_);
-            s.oid[k_] = wlane(s.oid[k_], oid, l_); s.tid[k_] = wlane(s.tid[k_], tid, l_);
-            s.ts[k_] = wlane(s.ts[k_], ts, l_); s.tns[k_] = wlane(s.tns[k_], tns, l_);)
+DEV i32 ldu(const i32* t, int R, int f, int e) { return uni(t[f * R + e]); }
+DEV void stu(i32* t, int R, int f, int e, i32 v) {
+    if (lane_id() == 0) t[f * R + e] = v;
+    lds_order();
 }
-template <int S> DEV void clear_slot(Side<S>& s, int e) { put_row(s, e, -1, -1, -1, -1, -1, -1); }
+DEV void st6(i32* t, int R, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5) {
+    const int l = lane_id();
+    i32 v = f0;
+    v = wlane(v, f1, 1); v = wlane(v, f2, 2); v = wlane(v, f3, 3); v = wlane(v, f4, 4); v = wlane(v, f5, 5);
+    if (l < 6) t[l * R + e] = v;
+    lds_order();
+}
+DEV void clr6(i32* t, int R, int e) {
+    const int l = lane_id();
+    if (l < 6) t[l * R + e] = -1;
+    lds_order();
+}
 // first slot over per-register lane masks; `fallback` if none
 template <int S> DEV int first_slot(const lmask (&m)[S], int fallback) {
     int idx = fallback;
@@ -249,103 +254,154 @@ template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
     for (int r = 0; r < S; ++r) m[r] = bal(pr[r]);
     return first_slot(m, fallback);
 }
+template <int S> DEV i32 sget(const i32 (&a)[S], int e) {
+    i32 v = 0;
+#pragma unroll
+    for (int k = 0; k < S; ++k)
+        if (S == 1 || (e >> 6) == k) v = rdl(a[k], e & 63);
+    return v;
+}
 
-template <int S> DEV void load_side(Side<S>& s, const i32* g, const Valid<S>& V) {
+template <int S>
+struct Side {
+    i32* t;              // LDS table [6][R]
+    // wave-uniform bookkeeping (SGPRs)
+    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid when ok
+    bool ok;             // cache valid
+    bool clean;          // every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
+                         // ever has to look at the row just written
+    bool neg1;           // some row with p != -1 holds a -1 in another field (then "first row
+                         // holding ANY -1" needs the full test, else p == -1 suffices)
+};
+
+// global [R][6] rows -> LDS side table, with the clean / neg1 flags
+template <int S> DEV void load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
+    const int l = lane_id();
+    lmask bad = 0, n1 = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const int sl = r * 64 + l;
+        i32 p = -1, q = -1, oid = -1, tid = -1, ts = -1, tns = -1;
+        if (V.v[r]) {
+            const int2* row = reinterpret_cast<const int2*>(g + sl * 6);
+            int2 x0 = row[0], x1 = row[1], x2 = row[2];
+            p = x0.x; q = x0.y; oid = x1.x; tid = x1.y; ts = x2.x; tns = x2.y;
+            i32* t = s.t + sl;
+            t[FP * R] = p; t[FQ * R] = q; t[FOID * R] = oid; t[FTID * R] = tid; t[FTS * R] = ts; t[FTNS * R] = tns;
+        }
+        const lmask any = bal(p == -1) | bal(q == -1) | bal(oid == -1) | bal(tid == -1) | bal(ts == -1) | bal(tns == -1);
+        const lmask all = bal(p == -1) & bal(q == -1) & bal(oid == -1) & bal(tid == -1) & bal(ts == -1) & bal(tns == -1);
+        bad |= V.m[r] & bal(q <= 0) & ~all;
+        n1 |= V.m[r] & ~bal(p == -1) & any;
+    }
+    lds_order();
+    s.clean = bad == 0ull;
+    s.neg1 = n1 != 0ull;
+    s.ok = false;
+}
+template <int S> DEV void store_side(const Side<S>& s, i32* g, int R, const Valid<S>& V) {
     const int l = lane_id();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         const int sl = r * 64 + l;
         if (V.v[r]) {
-            const int2* row = reinterpret_cast<const int2*>(g + sl * 6);
-            int2 x0 = row[0], x1 = row[1], x2 = row[2];
-            s.p[r] = x0.x; s.q[r] = x0.y; s.oid[r] = x1.x; s.tid[r] = x1.y; s.ts[r] = x2.x; s.tns[r] = x2.y;
-        } else {
-            s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
+            const i32* t = s.t + sl;
+            int2* row = reinterpret_cast<int2*>(g + sl * 6);
+            row[0] = make_int2(t[FP * R], t[FQ * R]);
+            row[1] = make_int2(t[FOID * R], t[FTID * R]);
+            row[2] = make_int2(t[FTS * R], t[FTNS * R]);
         }
     }
-    lmask bad = 0, n1 = 0;
-#pragma unroll
-    for (int r = 0; r < S; ++r) {
-        const lmask any = bal(s.p[r] == -1) | bal(s.q[r] == -1) | bal(s.oid[r] == -1) | bal(s.tid[r] == -1) |
-                          bal(s.ts[r] == -1) | bal(s.tns[r] == -1);
-        const lmask all = bal(s.p[r] == -1) & bal(s.q[r] == -1) & bal(s.oid[r] == -1) & bal(s.tid[r] == -1) &
-                          bal(s.ts[r] == -1) & bal(s.tns[r] == -1);
-        bad |= V.m[r] & bal(s.q[r] <= 0) & ~all;
-        n1 |= V.m[r] & ~bal(s.p[r] == -1) & any;
-    }
-    s.clean = bad == 0ull;
-    s.neg1 = n1 != 0ull;
-    s.ok = false;
 }
-template <int S> DEV void store_side(const Side<S>& s, i32* g, const Valid<S>& V) {
+// clear every valid slot whose field-f value is selected by lane mask m
+template <int S> DEV void clear_masked(i32* t, int R, const lmask (&m)[S]) {
     const int l = lane_id();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        if (V.v[r]) {
-            int2* row = reinterpret_cast<int2*>(g + (r * 64 + l) * 6);
-            row[0] = make_int2(s.p[r], s.q[r]);
-            row[1] = make_int2(s.oid[r], s.tid[r]);
-            row[2] = make_int2(s.ts[r], s.tns[r]);
+        if ((m[r] >> l) & 1ull) {
+#pragma unroll
+            for (int f = 0; f < 6; ++f) t[f * R + r * 64 + l] = -1;
         }
     }
+    lds_order();
 }
 
 // _removeZeroNegQuant — JaxOrderBookArrays.py:85-90, after row e was written
 // with quantity qe.  Clean side: only row e can hold q <= 0.
-template <int S> DEV void rzn(Side<S>& s, int e, i32 qe) {
+template <int S> DEV void rzn(Side<S>& s, int R, const Valid<S>& V, int e, i32 qe) {
     if (s.clean) {
-        if (qe <= 0) clear_slot(s, e);
+        if (qe <= 0) clr6(s.t, R, e);
     } else {
+        i32 q[S];
+        ldcol(s.t, R, FQ, q);
+        lmask m[S];
 #pragma unroll
-        for (int r = 0; r < S; ++r)
-            if (s.q[r] <= 0) s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
+        for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
+        clear_masked(s.t, R, m);
         s.clean = true;
         s.ok = false;
     }
 }
 
 // get_best_bid: max raw price (empty side -> -1); volume at it — :943-951,906-917
-template <int S> DEV void best_bid(Side<S>& s, const Valid<S>& V) {
+template <int S> DEV void best_bid_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i32& bp, i32& bq) {
     i32 m = INT_MIN;
 #pragma unroll
-    for (int r = 0; r < S; ++r) m = imax_(m, V.v[r] ? s.p[r] : INT_MIN);
+    for (int r = 0; r < S; ++r) m = imax_(m, V.v[r] ? p[r] : INT_MIN);
     const i32 mp = wave_max(m);
     i32 v = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] & (s.p[r] == mp)) ? s.q[r] : 0);
-    s.best_p = mp;
-    s.best_q = wave_sum(v);
-    s.ok = true;
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] & (p[r] == mp)) ? q[r] : 0);
+    bp = mp;
+    bq = wave_sum(v);
 }
 // get_best_ask: min price with -1 -> maxint, maxint -> -1; volume at it — :932-941
-template <int S> DEV void best_ask(Side<S>& s, const Valid<S>& V, i32 maxint) {
+template <int S>
+DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i32 maxint, i32& bp, i32& bq) {
     i32 m = INT_MAX;
 #pragma unroll
-    for (int r = 0; r < S; ++r) m = imin_(m, V.v[r] ? (s.p[r] == -1 ? maxint : s.p[r]) : INT_MAX);
-    i32 mn = wave_min(m);
+    for (int r = 0; r < S; ++r) m = imin_(m, V.v[r] ? (p[r] == -1 ? maxint : p[r]) : INT_MAX);
+    const i32 mn = wave_min(m);
     const i32 pa = mn == maxint ? -1 : mn;
     i32 v = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] & (s.p[r] == pa)) ? s.q[r] : 0);
-    s.best_p = pa;
-    s.best_q = wave_sum(v);
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] & (p[r] == pa)) ? q[r] : 0);
+    bp = pa;
+    bq = wave_sum(v);
+}
+template <int S> DEV void best_bid(Side<S>& s, int R, const Valid<S>& V) {
+    i32 p[S], q[S];
+    ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FQ, q);
+    best_bid_pq(p, q, V, s.best_p, s.best_q);
+    s.ok = true;
+}
+template <int S> DEV void best_ask(Side<S>& s, int R, const Valid<S>& V, i32 maxint) {
+    i32 p[S], q[S];
+    ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FQ, q);
+    best_ask_pq(p, q, V, maxint, s.best_p, s.best_q);
     s.ok = true;
 }
 
 // _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
 // mp is the side's max price (bid) / min price with -1 -> maxint (ask)
-template <bool BID, int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, const LobCfg& c, i32 mp) {
-    i32 t[S], n[S], m = INT_MAX;
+template <int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, const LobCfg& c, i32 mp) {
+    const int R = c.nO;
+    i32 p[S], ts[S], tns[S], t[S], n[S], m = INT_MAX;
+    ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FTS, ts);
+    ldcol(s.t, R, FTNS, tns);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        t[r] = (s.p[r] == mp) ? s.ts[r] : c.maxint;
+        t[r] = (p[r] == mp) ? ts[r] : c.maxint;
         m = imin_(m, V.v[r] ? t[r] : INT_MAX);
     }
     const i32 mts = wave_min(m);
     m = INT_MAX;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        n[r] = (t[r] == mts) ? s.tns[r] : c.maxint;
+        n[r] = (t[r] == mts) ? tns[r] : c.maxint;
         m = imin_(m, V.v[r] ? n[r] : INT_MAX);
     }
     const i32 mtn = wave_min(m);
@@ -356,65 +412,64 @@ template <bool BID, int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, 
 }
 
 // ------------------------------------------------------------ trade log
-// The trade log lives in LDS, structure-of-arrays [8 fields][64*S rows], so a
-// lane reads its rows' fields bank-conflict-free and appends (rare) touch one
-// row.  Keeping it out of VGPRs keeps the message loop at 4 waves/SIMD.
-template <int S>
+// LDS table [8 fields][R = nT rows]; appends (rare) touch one row.
 struct Trades {
-    i32* t;  // LDS base, 8 * 64 * S words
-    static constexpr int R = 64 * S;
+    i32* t;
+    int R;
     DEV i32 get(int k, int r) const { return t[k * R + r * 64 + lane_id()]; }
     DEV i32 at(int k, int row) const { return uni(t[k * R + row]); }
 };
-template <int S> DEV void trades_fill(Trades<S>& T, i32 v) {
+template <int S> DEV void trades_fill(Trades& T, const Valid<S>& V, i32 v) {
     const int l = lane_id();
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-        for (int r = 0; r < S; ++r) T.t[k * Trades<S>::R + r * 64 + l] = v;
-}
-template <int S> DEV void load_trades(Trades<S>& T, const i32* g, const Valid<S>& V) {
-    const int l = lane_id();
-#pragma unroll
-    for (int r = 0; r < S; ++r) {
-        int4 a = make_int4(-1, -1, -1, -1), b = a;
+    for (int r = 0; r < S; ++r)
         if (V.v[r]) {
-            const int4* row = reinterpret_cast<const int4*>(g + (r * 64 + l) * 8);
-            a = row[0];
-            b = row[1];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) T.t[k * T.R + r * 64 + l] = v;
         }
-        const int o = r * 64 + l, R = Trades<S>::R;
-        T.t[0 * R + o] = a.x; T.t[1 * R + o] = a.y; T.t[2 * R + o] = a.z; T.t[3 * R + o] = a.w;
-        T.t[4 * R + o] = b.x; T.t[5 * R + o] = b.y; T.t[6 * R + o] = b.z; T.t[7 * R + o] = b.w;
-    }
+    lds_order();
 }
-template <int S> DEV void store_trades(const Trades<S>& T, i32* g, const Valid<S>& V) {
+template <int S> DEV void load_trades(Trades& T, const i32* g, const Valid<S>& V) {
     const int l = lane_id();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         if (V.v[r]) {
-            const int o = r * 64 + l, R = Trades<S>::R;
-            int4* row = reinterpret_cast<int4*>(g + (r * 64 + l) * 8);
+            const int o = r * 64 + l, R = T.R;
+            const int4* row = reinterpret_cast<const int4*>(g + o * 8);
+            const int4 a = row[0], b = row[1];
+            T.t[0 * R + o] = a.x; T.t[1 * R + o] = a.y; T.t[2 * R + o] = a.z; T.t[3 * R + o] = a.w;
+            T.t[4 * R + o] = b.x; T.t[5 * R + o] = b.y; T.t[6 * R + o] = b.z; T.t[7 * R + o] = b.w;
+        }
+    }
+    lds_order();
+}
+template <int S> DEV void store_trades(const Trades& T, i32* g, const Valid<S>& V) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        if (V.v[r]) {
+            const int o = r * 64 + l, R = T.R;
+            int4* row = reinterpret_cast<int4*>(g + o * 8);
             row[0] = make_int4(T.t[0 * R + o], T.t[1 * R + o], T.t[2 * R + o], T.t[3 * R + o]);
             row[1] = make_int4(T.t[4 * R + o], T.t[5 * R + o], T.t[6 * R + o], T.t[7 * R + o]);
         }
     }
 }
 // write trade row e (uniform) — lanes 0..7 store one field each
-template <int S> DEV void trade_put(Trades<S>& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5, i32 f6,
-                                    i32 f7) {
+DEV void trade_put(Trades& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5, i32 f6, i32 f7) {
     const int l = lane_id();
     i32 v = f0;
-    v = l == 1 ? f1 : v; v = l == 2 ? f2 : v; v = l == 3 ? f3 : v;
-    v = l == 4 ? f4 : v; v = l == 5 ? f5 : v; v = l == 6 ? f6 : v; v = l == 7 ? f7 : v;
-    if (l < 8) T.t[l * Trades<S>::R + e] = v;
+    v = wlane(v, f1, 1); v = wlane(v, f2, 2); v = wlane(v, f3, 3);
+    v = wlane(v, f4, 4); v = wlane(v, f5, 5); v = wlane(v, f6, 6); v = wlane(v, f7, 7);
+    if (l < 8) T.t[l * T.R + e] = v;
+    lds_order();
 }
 
 // ------------------------------------------------------ message handlers
 template <int S>
 struct Book {
     Side<S> a, b;
-    Trades<S> tr;
+    Trades tr;
     Valid<S> vs, vt;
     LobCfg c;
 };
@@ -451,8 +506,9 @@ template <int S> DEV void note_reduce(Side<S>& s, i32 op, i32 dq) {
 
 // match_order — JaxOrderBookArrays.py:172-220
 template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
-    i32 qt = 0, pt = 0, ot = 0, tt = 0;
-    ON_SLOT(S, top, qt = rdl(s.q[k_], l_); pt = rdl(s.p[k_], l_); ot = rdl(s.oid[k_], l_); tt = rdl(s.tid[k_], l_);)
+    const int R = B.c.nO;
+    const i32 qt = ldu(s.t, R, FQ, top), pt = ldu(s.t, R, FP, top);
+    const i32 ot = ldu(s.t, R, FOID, top), tt = ldu(s.t, R, FTID, top);
     const i32 newq = imax_(0, wsub(qt, qtm));
     const i32 rem = wsub(qtm, qt);
     lmask fm[S];
@@ -461,12 +517,12 @@ template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, c
     const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
     if (s.clean) {
-        if (newq <= 0) clear_slot(s, top);
-        else sset(s.q, top, newq);
+        if (newq <= 0) clr6(s.t, R, top);
+        else stu(s.t, R, FQ, top, newq);
         note_reduce(s, pt, wsub(qt, newq));
     } else {
-        sset(s.q, top, newq);
-        rzn(s, top, newq);
+        stu(s.t, R, FQ, top, newq);
+        rzn(s, R, B.vs, top, newq);
     }
     return rem;
 }
@@ -476,11 +532,11 @@ template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, c
 // a crossing best pays for the 3-reduction top-of-book.
 template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     while (qtm > 0) {
-        if (!s.ok) { if (BID) best_bid(s, B.vs); else best_ask(s, B.vs, B.c.maxint); }
+        if (!s.ok) { if (BID) best_bid(s, B.c.nO, B.vs); else best_ask(s, B.c.nO, B.vs, B.c.maxint); }
         const i32 mp = BID ? s.best_p : (s.best_p == -1 ? B.c.maxint : s.best_p);
         if (BID ? !(mp >= price) : !(mp <= price)) break;
-        const int top = top_idx<BID>(s, B.vs, B.c, mp);
-        const i32 tp = sget(s.p, top);
+        const int top = top_idx(s, B.vs, B.c, mp);
+        const i32 tp = ldu(s.t, B.c.nO, FP, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
         qtm = match_order(B, s, top, qtm, m);
     }
@@ -489,52 +545,61 @@ template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
 template <bool BID, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
+    const int R = B.c.nO;
     lmask fm[S];
+    i32 p[S];
+    ldcol(s.t, R, FP, p);
     const bool fast = s.clean && !s.neg1;  // then "any -1" <=> p == -1
     if (fast) {
 #pragma unroll
-        for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(s.p[r] == -1);
+        for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == -1);
     } else {
+        i32 q[S], o[S], t[S], ts[S], tn[S];
+        ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
+        ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
 #pragma unroll
         for (int r = 0; r < S; ++r)
-            fm[r] = B.vs.m[r] & (bal(s.p[r] == -1) | bal(s.q[r] == -1) | bal(s.oid[r] == -1) |
-                                 bal(s.tid[r] == -1) | bal(s.ts[r] == -1) | bal(s.tns[r] == -1));
+            fm[r] = B.vs.m[r] & (bal(p[r] == -1) | bal(q[r] == -1) | bal(o[r] == -1) | bal(t[r] == -1) |
+                                 bal(ts[r] == -1) | bal(tn[r] == -1));
     }
-    const int e = first_slot(fm, B.c.nO - 1);
+    const int e = first_slot(fm, R - 1);
     const i32 nq = imax_(0, qty);
     if (!s.clean) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
-        put_row(s, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        rzn(s, e, nq);
+        st6(s.t, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        rzn(s, R, B.vs, e, nq);
         return;
     }
-    i32 op = 0, oq = 0;
-    ON_SLOT(S, e, op = rdl(s.p[k_], l_); oq = rdl(s.q[k_], l_);)
+    const i32 op = sget(p, e), oq = ldu(s.t, R, FQ, e);
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
-        put_row(s, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        st6(s.t, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1))) s.neg1 = true;
         if (was_empty) note_add<BID>(s, m.price, nq, B.c.maxint);
         else s.ok = false;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
-        clear_slot(s, e);
+        clr6(s.t, R, e);
         s.ok = false;
     }
 }
 
 // check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max)
 template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
+    const int R = B.c.nO;
+    i32 p[S];
+    ldcol(s.t, R, FP, p);
     lmask neg = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(s.p[r] < 0);
+    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(p[r] < 0);
     if (neg != 0ull) return;
     i32 w = BID ? INT_MAX : INT_MIN;
 #pragma unroll
     for (int r = 0; r < S; ++r)
-        w = BID ? imin_(w, B.vs.v[r] ? s.p[r] : INT_MAX) : imax_(w, B.vs.v[r] ? s.p[r] : INT_MIN);
+        w = BID ? imin_(w, B.vs.v[r] ? p[r] : INT_MAX) : imax_(w, B.vs.v[r] ? p[r] : INT_MIN);
     const i32 worst = BID ? wave_min(w) : wave_max(w);
+    lmask m[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r)
-        if (s.p[r] == worst) s.p[r] = s.q[r] = s.oid[r] = s.tid[r] = s.ts[r] = s.tns[r] = -1;
+    for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(p[r] == worst);
+    clear_masked(s.t, R, m);
     s.ok = false;
 }
 
@@ -556,28 +621,33 @@ template <int S> DEV void ask_lim(Book<S>& B, Msg m) {
 }
 // cancel_order + get_init_id_match — :93-139
 template <int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+    const int R = B.c.nO;
+    i32 o[S];
+    ldcol(s.t, R, FOID, o);
     lmask fm[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(s.oid[r] == m.oid);
+    for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
     int idx = first_slot(fm, -1);
     if (idx < 0) {
+        i32 p[S], q[S];
+        ldcol(s.t, R, FP, p);
+        ldcol(s.t, R, FQ, q);
         const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
 #pragma unroll
         for (int r = 0; r < S; ++r)
-            fm[r] = B.vs.m[r] & bal(s.p[r] == m.price) & bal(s.oid[r] <= B.c.init_id) & bal(s.oid[r] >= lo) &
-                    bal(s.q[r] >= m.qty);
-        idx = first_slot(fm, B.c.nO - 1);  // -1 wraps to the last slot
+            fm[r] = B.vs.m[r] & bal(p[r] == m.price) & bal(o[r] <= B.c.init_id) & bal(o[r] >= lo) &
+                    bal(q[r] >= m.qty);
+        idx = first_slot(fm, R - 1);  // -1 wraps to the last slot
     }
-    i32 op = 0, oq = 0;
-    ON_SLOT(S, idx, op = rdl(s.p[k_], l_); oq = rdl(s.q[k_], l_);)
+    const i32 op = ldu(s.t, R, FP, idx), oq = ldu(s.t, R, FQ, idx);
     const i32 nq = wsub(oq, m.qty);
     if (s.clean) {
-        if (nq <= 0) clear_slot(s, idx);
-        else sset(s.q, idx, nq);
+        if (nq <= 0) clr6(s.t, R, idx);
+        else stu(s.t, R, FQ, idx, nq);
         note_reduce(s, op, wsub(oq, nq > 0 ? nq : 0));
     } else {
-        sset(s.q, idx, nq);
-        rzn(s, idx, nq);
+        stu(s.t, R, FQ, idx, nq);
+        rzn(s, R, B.vs, idx, nq);
     }
 }
 
@@ -596,31 +666,40 @@ template <int S> DEV void process_msg(Book<S>& B, i32 d0, i32 d1, i32 d2, i32 d3
     else if (!((d0 == 0) & (m.side == 0))) ask_lim(B, m);
 }
 template <int S> DEV void refresh_best(Book<S>& B) {
-    if (!B.a.ok) best_ask(B.a, B.vs, B.c.maxint);
-    if (!B.b.ok) best_bid(B.b, B.vs);
+    if (!B.a.ok) best_ask(B.a, B.c.nO, B.vs, B.c.maxint);
+    if (!B.b.ok) best_bid(B.b, B.c.nO, B.vs);
+}
+
+// LDS carve-up of one env's book: [asks 6*nO][bids 6*nO][trades 8*nT][pad 64*4]
+template <int S> DEV void book_bind(Book<S>& B, i32* lds) {
+    B.a.t = lds;
+    B.b.t = lds + 6 * B.c.nO;
+    B.tr.t = lds + 12 * B.c.nO;
+    B.tr.R = B.c.nT;
+    B.vs.init(B.c.nO);
+    B.vt.init(B.c.nT);
 }
 
 // ================================================= K1: book_process kernel
 // scan_through_entire_array[_save_bidask] — JaxOrderBookArrays.py:736-823
 template <int S>
-__global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
+__global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
                                                      i32* __restrict__ asks, i32* __restrict__ bids,
                                                      i32* __restrict__ trades, i32* __restrict__ best_asks,
                                                      i32* __restrict__ best_bids) {
+    extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
-    __shared__ i32 trade_lds[8 * 64 * S];
     const int l = lane_id();
     Book<S> B;
-    B.tr.t = trade_lds;
     B.c = lobcfg(cfg);
-    B.vs.init(B.c.nO);
-    B.vt.init(B.c.nT);
-    i32* ga = asks + (size_t)e * B.c.nO * 6;
-    i32* gb = bids + (size_t)e * B.c.nO * 6;
+    book_bind(B, lds);
+    const int R = B.c.nO;
+    i32* ga = asks + (size_t)e * R * 6;
+    i32* gb = bids + (size_t)e * R * 6;
     i32* gt = trades + (size_t)e * B.c.nT * 8;
-    load_side(B.a, ga, B.vs);
-    load_side(B.b, gb, B.vs);
+    load_side(B.a, ga, R, B.vs);
+    load_side(B.b, gb, R, B.vs);
     load_trades(B.tr, gt, B.vt);
     const i32* gm = msgs + (size_t)e * n_msg * 8;
     for (int base = 0; base < n_msg; base += 64) {
@@ -637,8 +716,8 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_book_process(hftlob_lo
                         rdl(y.z, k), rdl(y.w, k));
             if (best_asks) {
                 refresh_best(B);
-                ap = wrl(ap, B.a.best_p, k); aq = wrl(aq, B.a.best_q, k);
-                bp = wrl(bp, B.b.best_p, k); bq = wrl(bq, B.b.best_q, k);
+                ap = wlane(ap, B.a.best_p, k); aq = wlane(aq, B.a.best_q, k);
+                bp = wlane(bp, B.b.best_p, k); bq = wlane(bq, B.b.best_q, k);
             }
         }
         if (best_asks && row < n_msg) {
@@ -646,8 +725,8 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_book_process(hftlob_lo
             reinterpret_cast<int2*>(best_bids + ((size_t)e * n_msg + row) * 2)[0] = make_int2(bp, bq);
         }
     }
-    store_side(B.a, ga, B.vs);
-    store_side(B.b, gb, B.vs);
+    store_side(B.a, ga, R, B.vs);
+    store_side(B.b, gb, R, B.vs);
     store_trades(B.tr, gt, B.vt);
 }
 
@@ -663,11 +742,29 @@ enum { W_T0 = 0, W_T1, W_OIDC, W_MID, W_DT };
 DEV int agent_words(const hftlob_agent_type_cfg& t) { return t.kind == HFTLOB_AGENT_MM ? 5 : 13; }
 
 // side volume (get_volume — :919-930)
-template <int S> DEV i32 side_volume(const Side<S>& s, const Valid<S>& V) {
+template <int S> DEV i32 side_volume_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V) {
     i32 v = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.p[r] != -1) ? s.q[r] : 0);
+    for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && p[r] != -1) ? q[r] : 0);
     return wave_sum(v);
+}
+template <int S> DEV i32 side_volume(const Side<S>& s, int R, const Valid<S>& V) {
+    i32 p[S], q[S];
+    ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FQ, q);
+    return side_volume_pq(p, q, V);
+}
+// prices and quantities of a global [R][6] side, lane-strided into registers
+template <int S> DEV void global_pq(const i32* g, const Valid<S>& V, i32 (&p)[S], i32 (&q)[S]) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        p[r] = q[r] = -1;
+        if (V.v[r]) {
+            const int2 x = reinterpret_cast<const int2*>(g + (r * 64 + l) * 6)[0];
+            p[r] = x.x; q[r] = x.y;
+        }
+    }
 }
 
 // canonical float sum of per-row values over n rows held S-strided
@@ -770,25 +867,25 @@ DEV void env_reset_dev(const hftlob_env_cfg& c, Key key, const i32* __restrict__
             for (int k = w; k < c.init_rec_words; ++k) rec[k] = src[k];
         }
     }
-    Side<S> a, b;
-    load_side(a, src + c.off_asks, VS);
-    load_side(b, src + c.off_bids, VS);
-    best_ask(a, VS, c.lob.maxint);
-    best_bid(b, VS);
+    i32 ap[S], aq[S], bp[S], bq[S], ba_p, ba_q, bb_p, bb_q;
+    global_pq(src + c.off_asks, VS, ap, aq);
+    global_pq(src + c.off_bids, VS, bp, bq);
+    best_ask_pq(ap, aq, VS, c.lob.maxint, ba_p, ba_q);
+    best_bid_pq(bp, bq, VS, bb_p, bb_q);
     // tile best quotes over M rows
     for (int m = l; m < c.n_msgs; m += 64) {
-        reinterpret_cast<int2*>(rec + c.off_best_asks)[m] = make_int2(a.best_p, a.best_q);
-        reinterpret_cast<int2*>(rec + c.off_best_bids)[m] = make_int2(b.best_p, b.best_q);
+        reinterpret_cast<int2*>(rec + c.off_best_asks)[m] = make_int2(ba_p, ba_q);
+        reinterpret_cast<int2*>(rec + c.off_best_bids)[m] = make_int2(bb_p, bb_q);
     }
-    const float mid = i2f(wadd(b.best_p, a.best_p)) / 2.0f;
+    const float mid = i2f(wadd(bb_p, ba_p)) / 2.0f;
     const i32 t0 = src[c.off_loaded + LD_T0], t1 = src[c.off_loaded + LD_T1];
     if (l == 0) {
         i32* W = rec + c.off_world;
         W[W_T0] = t0; W[W_T1] = t1; W[W_OIDC] = c.order_id_counter_start; W[W_MID] = fbit(mid); W[W_DT] = fbit(0.0f);
     }
     WorldView wv;
-    wv.best_ask_p = a.best_p; wv.best_bid_p = b.best_p;
-    wv.vol_a = side_volume(a, VS); wv.vol_b = side_volume(b, VS);
+    wv.best_ask_p = ba_p; wv.best_bid_p = bb_p;
+    wv.vol_a = side_volume_pq(ap, aq, VS); wv.vol_b = side_volume_pq(bp, bq, VS);
     wv.step = src[c.off_loaded + LD_STEP]; wv.max_steps = src[c.off_loaded + LD_MAXS]; wv.mid = mid;
     // zero the record's padding words (after the world block, after the agents)
     int agents_end = c.off_agents;
@@ -851,17 +948,19 @@ DEV i32 get_field(const i32* lds_rows, int row, int f) { return uni(lds_rows[row
 
 // getCancelMsgs — JaxOrderBookArrays.py:827-853
 template <int S>
-DEV void cancel_rows(const Side<S>& s, const Valid<S>& V, i32 agent, int size, i32 side, i32 t, i32 tns,
+DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int size, i32 side, i32 t, i32 tns,
                      i32* lds_rows, int row0) {
     int n = 0;
+    i32 tid[S];
+    ldcol(s.t, R, FTID, tid);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        unsigned long long bm = V.m[r] & bal(s.tid[r] == agent);
+        lmask bm = V.m[r] & bal(tid[r] == agent);
         while (bm && n < size) {
-            const int l = (int)__builtin_ctzll(bm);
+            const int e = r * 64 + (int)__builtin_ctzll(bm);
             bm &= bm - 1;
-            put_row(lds_rows, row0 + n, 2, side, rdl(s.q[r], l), rdl(s.p[r], l), rdl(s.oid[r], l),
-                    rdl(s.tid[r], l), t, tns);
+            put_row(lds_rows, row0 + n, 2, side, ldu(s.t, R, FQ, e), ldu(s.t, R, FP, e), ldu(s.t, R, FOID, e),
+                    agent, t, tns);
             ++n;
         }
     }
@@ -925,11 +1024,13 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
     if (tc.fixed_action_setting) action = tc.fixed_action;
     const i32 tick = c.tick_size;
     // best ask / bid of the book with the agent's own orders masked out
-    i32 mn = INT_MAX, mx = INT_MIN;
+    i32 mn = INT_MAX, mx = INT_MIN, ap_[S], at_[S], bp_[S], bt_[S];
+    ldcol(B.a.t, B.c.nO, FP, ap_); ldcol(B.a.t, B.c.nO, FTID, at_);
+    ldcol(B.b.t, B.c.nO, FP, bp_); ldcol(B.b.t, B.c.nO, FTID, bt_);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        const i32 pa = (B.vs.v[r] && B.a.tid[r] != tid) ? B.a.p[r] : -1;
-        const i32 pb = (B.vs.v[r] && B.b.tid[r] != tid) ? B.b.p[r] : -1;
+        const i32 pa = (B.vs.v[r] && at_[r] != tid) ? ap_[r] : -1;
+        const i32 pb = (B.vs.v[r] && bt_[r] != tid) ? bp_[r] : -1;
         mn = imin_(mn, B.vs.v[r] ? (pa == -1 ? c.lob.maxint : pa) : INT_MAX);
         mx = imax_(mx, B.vs.v[r] ? pb : INT_MIN);
     }
@@ -1303,15 +1404,13 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
 template <int S, int NFIX>
-__global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
+__global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
                                                  const i32* __restrict__ actions, const i32* __restrict__ msg_data,
                                                  const i32* __restrict__ init_states, i32* __restrict__ state,
                                                  float* __restrict__ obs_out, float* __restrict__ rew_out,
                                                  i32* __restrict__ done_all_out, i32* __restrict__ dones_out,
                                                  i32* __restrict__ info_out) {
-    __shared__ __attribute__((aligned(16))) i32 rows[MAX_AGENT_ROWS * 8];
-    __shared__ i32 axs[HFTLOB_MAX_AGENTS * 6];  // per-agent action extras
-    __shared__ i32 trade_lds[8 * 64 * S];
+    extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
     STAMP(t_start);
@@ -1319,12 +1418,14 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cf
     const bool part = c.prng_partitionable;
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
     i32* rec = state + (size_t)e * c.rec_words;
+    // LDS: [agent rows (C+A)*8][action extras n_agents*6, 16B-padded][book]
+    i32* rows = lds;
+    i32* axs = rows + (C + A) * 8;
     Book<S> B;
-    B.tr.t = trade_lds;
     B.c = lobcfg(c.lob);
     if (NFIX > 0) { B.c.nO = NFIX; B.c.nT = NFIX; }
-    B.vs.init(B.c.nO);
-    B.vt.init(B.c.nT);
+    const int R = B.c.nO;
+    book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
     const Key key{keys[2 * e], keys[2 * e + 1]};
     const Key k1 = split_key(key, 2, 0, part), key_reset = split_key(key, 2, 1, part);
     // loaded / world scalars (wave-uniform)
@@ -1346,8 +1447,8 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cf
             excl_any = ballot(any) != 0ull;
         }
     }
-    load_side(B.a, rec + c.off_asks, B.vs);
-    load_side(B.b, rec + c.off_bids, B.vs);
+    load_side(B.a, rec + c.off_asks, R, B.vs);
+    load_side(B.b, rec + c.off_bids, R, B.vs);
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
     {
@@ -1366,12 +1467,12 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cf
                     else
                         mm_fixed_quant(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
                     const int sz = tc.n_msgs / 4;
-                    cancel_rows(B.b, B.vs, tid, sz, 1, wt0, wt1, rows, crow);
-                    cancel_rows(B.a, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
+                    cancel_rows(B.b, R, B.vs, tid, sz, 1, wt0, wt1, rows, crow);
+                    cancel_rows(B.a, R, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
                 } else {
                     exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow);
                     const i32 sell = s4[3];
-                    cancel_rows(sell ? B.a : B.b, B.vs, tid, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
+                    cancel_rows(sell ? B.a : B.b, R, B.vs, tid, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
                                 crow);
                 }
                 {
@@ -1421,7 +1522,7 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cf
 
     STAMP(t_agents);
     // ---- (B)+(D) stream the combined messages through the book, 64 per chunk
-    trades_fill(B.tr, -1);
+    trades_fill(B.tr, B.vt, -1);
     i32 dstart = wadd(start_index, wmul(D, step));
     dstart = imax_(0, imin_(dstart, c.n_data_rows - D));  // dynamic_slice clamping
     const int AR = C + A;
@@ -1457,8 +1558,8 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cf
             if (pb == -1) qb = 0;
             if (pa != -1) prev_a = pa;
             if (pb != -1) prev_b = pb;
-            cap = wrl(cap, prev_a, k); caq = wrl(caq, qa, k);
-            cbp = wrl(cbp, prev_b, k); cbq = wrl(cbq, qb, k);
+            cap = wlane(cap, prev_a, k); caq = wlane(caq, qa, k);
+            cbp = wlane(cbp, prev_b, k); cbq = wlane(cbq, qb, k);
         }
         if (row < M) {
             reinterpret_cast<int2*>(rec + c.off_best_asks)[row] = make_int2(cap, caq);
@@ -1489,11 +1590,11 @@ __global__ __launch_bounds__(64, (S <= 2 ? 4 : 2)) void k_env_step(hftlob_env_cf
     // ---- (E) rewards, (G) agent states, (K) observations
     WorldView wv;
     wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
-    wv.vol_a = side_volume(B.a, B.vs); wv.vol_b = side_volume(B.b, B.vs);
+    wv.vol_a = side_volume(B.a, R, B.vs); wv.vol_b = side_volume(B.b, R, B.vs);
     // the book is final: store it now (frees its registers for the rewards);
     // an auto-reset below overwrites the record anyway
-    store_side(B.a, rec + c.off_asks, B.vs);
-    store_side(B.b, rec + c.off_bids, B.vs);
+    store_side(B.a, rec + c.off_asks, R, B.vs);
+    store_side(B.b, rec + c.off_bids, R, B.vs);
     store_trades(B.tr, rec + c.off_trades, B.vt);
     wv.step = wadd(step, 1); wv.max_steps = max_steps; wv.mid = X.last_mid;
     i32* info = info_out ? info_out + (size_t)e * c.info_words : nullptr;
@@ -1659,9 +1760,10 @@ int hftlob_book_process(const hftlob_lob_cfg* cfg, int n_env, int n_msg, const i
     const int S = slot_sets(cfg->n_orders > cfg->n_trades ? cfg->n_orders : cfg->n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
-    if (S == 1) hipLaunchKernelGGL(k_book_process<1>, g, b, 0, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
-    else if (S == 2) hipLaunchKernelGGL(k_book_process<2>, g, b, 0, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
-    else hipLaunchKernelGGL(k_book_process<4>, g, b, 0, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+    const size_t shm = 4 * ((size_t)12 * cfg->n_orders + 8 * cfg->n_trades + 64 * 4);
+    if (S == 1) hipLaunchKernelGGL(k_book_process<1>, g, b, shm, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+    else if (S == 2) hipLaunchKernelGGL(k_book_process<2>, g, b, shm, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+    else hipLaunchKernelGGL(k_book_process<4>, g, b, shm, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
     return launch_status();
 }
 
@@ -1723,7 +1825,9 @@ int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, 
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
-#define LAUNCH_STEP(SS, NF) hipLaunchKernelGGL((k_env_step<SS, NF>), g, b, 0, st, *cfg, n_env, keys, actions, msg_data, \
+    const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
+                            12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+#define LAUNCH_STEP(SS, NF) hipLaunchKernelGGL((k_env_step<SS, NF>), g, b, shm, st, *cfg, n_env, keys, actions, msg_data, \
                                                init_states, state, out->obs, out->rewards, out->done_all, out->dones, \
                                                out->info)
     if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100);
