@@ -225,20 +225,25 @@ template <int S> DEV void ldcol(const i32* t, int R, int f, i32 (&o)[S]) {
     for (int r = 0; r < S; ++r) o[r] = t[f * R + r * 64 + l];
 }
 DEV i32 ldu(const i32* t, int R, int f, int e) { return uni(t[f * R + e]); }
-DEV void stu(i32* t, int R, int f, int e, i32 v) {
-    if (lane_id() == 0) t[f * R + e] = v;
+// Slot writes: every lane stores, the lanes that are not writing a field
+// store into their own word of a 64-word scratch row (`scr`).  That keeps
+// the exec mask untouched (no s_and_saveexec / s_or pair per store), which
+// matters because the scalar unit is the shared resource of a CU.
+DEV void stu(i32* t, i32* scr, int R, int f, int e, i32 v) {
+    const int l = lane_id();
+    *(l == 0 ? t + f * R + e : scr + l) = v;
     lds_order();
 }
-DEV void st6(i32* t, int R, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5) {
+DEV void st6(i32* t, i32* scr, int R, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5) {
     const int l = lane_id();
     i32 v = f0;
     v = wlane(v, f1, 1); v = wlane(v, f2, 2); v = wlane(v, f3, 3); v = wlane(v, f4, 4); v = wlane(v, f5, 5);
-    if (l < 6) t[l * R + e] = v;
+    *(l < 6 ? t + l * R + e : scr + l) = v;
     lds_order();
 }
-DEV void clr6(i32* t, int R, int e) {
+DEV void clr6(i32* t, i32* scr, int R, int e) {
     const int l = lane_id();
-    if (l < 6) t[l * R + e] = -1;
+    *(l < 6 ? t + l * R + e : scr + l) = -1;
     lds_order();
 }
 // first slot over per-register lane masks; `fallback` if none
@@ -265,6 +270,7 @@ template <int S> DEV i32 sget(const i32 (&a)[S], int e) {
 template <int S>
 struct Side {
     i32* t;              // LDS table [6][R]
+    i32* scr;            // LDS scratch row (64 words)
     // wave-uniform bookkeeping (SGPRs)
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid when ok
     bool ok;             // cache valid
@@ -330,7 +336,7 @@ template <int S> DEV void clear_masked(i32* t, int R, const lmask (&m)[S]) {
 // with quantity qe.  Clean side: only row e can hold q <= 0.
 template <int S> DEV void rzn(Side<S>& s, int R, const Valid<S>& V, int e, i32 qe) {
     if (s.clean) {
-        if (qe <= 0) clr6(s.t, R, e);
+        if (qe <= 0) clr6(s.t, s.scr, R, e);
     } else {
         i32 q[S];
         ldcol(s.t, R, FQ, q);
@@ -415,6 +421,7 @@ template <int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, const LobC
 // LDS table [8 fields][R = nT rows]; appends (rare) touch one row.
 struct Trades {
     i32* t;
+    i32* scr;
     int R;
     DEV i32 get(int k, int r) const { return t[k * R + r * 64 + lane_id()]; }
     DEV i32 at(int k, int row) const { return uni(t[k * R + row]); }
@@ -461,7 +468,7 @@ DEV void trade_put(Trades& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32
     i32 v = f0;
     v = wlane(v, f1, 1); v = wlane(v, f2, 2); v = wlane(v, f3, 3);
     v = wlane(v, f4, 4); v = wlane(v, f5, 5); v = wlane(v, f6, 6); v = wlane(v, f7, 7);
-    if (l < 8) T.t[l * T.R + e] = v;
+    *(l < 8 ? T.t + l * T.R + e : T.scr + l) = v;
     lds_order();
 }
 
@@ -475,7 +482,7 @@ struct Book {
 };
 
 struct Msg {
-    i32 type, side, price, qty, oid, tid, t, tns;
+    i32 side, price, qty, oid, tid, t, tns;
 };
 
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
@@ -517,11 +524,11 @@ template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, c
     const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
     if (s.clean) {
-        if (newq <= 0) clr6(s.t, R, top);
-        else stu(s.t, R, FQ, top, newq);
+        if (newq <= 0) clr6(s.t, s.scr, R, top);
+        else stu(s.t, s.scr, R, FQ, top, newq);
         note_reduce(s, pt, wsub(qt, newq));
     } else {
-        stu(s.t, R, FQ, top, newq);
+        stu(s.t, s.scr, R, FQ, top, newq);
         rzn(s, R, B.vs, top, newq);
     }
     return rem;
@@ -565,19 +572,19 @@ template <bool BID, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg&
     const int e = first_slot(fm, R - 1);
     const i32 nq = imax_(0, qty);
     if (!s.clean) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
-        st6(s.t, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         rzn(s, R, B.vs, e, nq);
         return;
     }
     const i32 op = sget(p, e), oq = ldu(s.t, R, FQ, e);
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
-        st6(s.t, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1))) s.neg1 = true;
         if (was_empty) note_add<BID>(s, m.price, nq, B.c.maxint);
         else s.ok = false;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
-        clr6(s.t, R, e);
+        clr6(s.t, s.scr, R, e);
         s.ok = false;
     }
 }
@@ -603,20 +610,18 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
     s.ok = false;
 }
 
-// bid_lim — :357-420
-template <int S> DEV void bid_lim(Book<S>& B, Msg m) {
+// bid_lim — :357-420 (discard: a type-4 message under type_4_interpretation 0/2)
+template <int S> DEV void bid_lim(Book<S>& B, Msg m, bool discard) {
     const i32 rem = match_against<false>(B, B.a, m.qty, m.price, m);
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
     if (B.c.check_fill) evict_if_full<true>(B, B.b);
-    const bool discard = (B.c.t4 == 0 || B.c.t4 == 2) && m.type == 4;
     if (!discard) add_order<true>(B, B.b, m, rem);
 }
 // ask_lim — :446-508
-template <int S> DEV void ask_lim(Book<S>& B, Msg m) {
+template <int S> DEV void ask_lim(Book<S>& B, Msg m, bool discard) {
     if (B.c.t4 == 2) m.price = 0;
     const i32 rem = match_against<true>(B, B.b, m.qty, m.price, m);
     if (B.c.check_fill) evict_if_full<false>(B, B.a);
-    const bool discard = (B.c.t4 == 0 || B.c.t4 == 2) && m.type == 4;
     if (!discard) add_order<false>(B, B.a, m, rem);
 }
 // cancel_order + get_init_id_match — :93-139
@@ -642,28 +647,50 @@ template <int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     const i32 op = ldu(s.t, R, FP, idx), oq = ldu(s.t, R, FQ, idx);
     const i32 nq = wsub(oq, m.qty);
     if (s.clean) {
-        if (nq <= 0) clr6(s.t, R, idx);
-        else stu(s.t, R, FQ, idx, nq);
+        if (nq <= 0) clr6(s.t, s.scr, R, idx);
+        else stu(s.t, s.scr, R, FQ, idx, nq);
         note_reduce(s, op, wsub(oq, nq > 0 ? nq : 0));
     } else {
-        stu(s.t, R, FQ, idx, nq);
+        stu(s.t, s.scr, R, FQ, idx, nq);
         rzn(s, R, B.vs, idx, nq);
     }
 }
 
 // cond_type_side_save_bidask — :687-732: dispatch index
 //   1 side==1 & type in {1,4}; 2 side==-1 & type in {2,3}; 3 side==1 & type in {2,3};
-//   4 side==0 & type==0 (doNothing); everything else 0 (ask_lim); side flipped for type 4
-template <int S> DEV void process_msg(Book<S>& B, i32 d0, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+//   4 side==0 & type==0 (doNothing); everything else 0 (ask_lim); side flipped for type 4.
+// Evaluated in VALU for the 64 messages of a chunk at once (lane = message):
+// x = (type, side, qty, price) becomes (handler | H_DISCARD, side', qty, price).
+enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8 };
+DEV void decode_msgs(const LobCfg& c, int4& x) {
+    const i32 ty = x.x, sd = ty == 4 ? wsub(0, x.y) : x.y;
+    const bool cnl = (ty == 2) | (ty == 3);
+    i32 h = H_ASK;
+    h = (((ty == 0) & (sd == 0))) ? H_NOP : h;
+    h = (((ty == 1) | (ty == 4)) & (sd == 1)) ? H_BID : h;
+    h = (cnl & (sd == 1)) ? H_CNL_BID : h;
+    h = (cnl & (sd == -1)) ? H_CNL_ASK : h;
+    if (((c.t4 == 0) | (c.t4 == 2)) & (ty == 4)) h |= H_DISCARD;
+    x.x = h;
+    x.y = sd;
+}
+template <int S> DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
-    m.type = d0;
-    m.side = d0 == 4 ? wsub(0, d1) : d1;
-    m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
-    const bool cnl = (d0 == 2) | (d0 == 3);
-    if (cnl & (m.side == -1)) cancel(B, B.a, m);
-    else if (cnl & (m.side == 1)) cancel(B, B.b, m);
-    else if (((d0 == 1) | (d0 == 4)) & (m.side == 1)) bid_lim(B, m);
-    else if (!((d0 == 0) & (m.side == 0))) ask_lim(B, m);
+    m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
+    const i32 kind = h & H_KIND;
+    const bool disc = (h & H_DISCARD) != 0;
+    if (kind == H_CNL_ASK) cancel(B, B.a, m);
+    else if (kind == H_CNL_BID) cancel(B, B.b, m);
+    else if (kind == H_BID) bid_lim(B, m, disc);
+    else if (kind == H_ASK) ask_lim(B, m, disc);
+}
+// forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
+DEV i32 ffill(i32 v, i32 carry) {
+    const int l = lane_id();
+    const lmask m = bal(v != -1) & (~0ull >> (63 - l));  // lanes <= l holding a price
+    const int src = m ? 63 - __builtin_clzll(m) : -1;
+    const i32 got = __builtin_amdgcn_ds_bpermute(src << 2, v);
+    return src < 0 ? carry : got;
 }
 template <int S> DEV void refresh_best(Book<S>& B) {
     if (!B.a.ok) best_ask(B.a, B.c.nO, B.vs, B.c.maxint);
@@ -671,11 +698,14 @@ template <int S> DEV void refresh_best(Book<S>& B) {
 }
 
 // LDS carve-up of one env's book: [asks 6*nO][bids 6*nO][trades 8*nT][pad 64*4]
+// (column loads may over-read up to 127 words past the trades: padding; the
+// last 64 pad words are the store scratch row)
 template <int S> DEV void book_bind(Book<S>& B, i32* lds) {
     B.a.t = lds;
     B.b.t = lds + 6 * B.c.nO;
     B.tr.t = lds + 12 * B.c.nO;
     B.tr.R = B.c.nT;
+    B.a.scr = B.b.scr = B.tr.scr = lds + 12 * B.c.nO + 8 * B.c.nT + 192;
     B.vs.init(B.c.nO);
     B.vt.init(B.c.nT);
 }
@@ -709,6 +739,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
             x = reinterpret_cast<const int4*>(gm + row * 8)[0];
             y = reinterpret_cast<const int4*>(gm + row * 8)[1];
         }
+        decode_msgs(B.c, x);
         i32 ap = 0, aq = 0, bp = 0, bq = 0;
         const int cnt = imin_(64, n_msg - base);
         for (int k = 0; k < cnt; ++k) {
@@ -1541,26 +1572,27 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             x = reinterpret_cast<const int4*>(g)[0];
             y = reinterpret_cast<const int4*>(g)[1];
         }
-        i32 cap = 0, caq = 0, cbp = 0, cbq = 0;
+        decode_msgs(B.c, x);
+        i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
         const int cnt = imin_(64, M - base);
         for (int k = 0; k < cnt; ++k) {
             process_msg(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k), rdl(y.z, k),
                         rdl(y.w, k));
             refresh_best(B);
-            // abort flag on raw quotes; _ffill_best_prices (marl_env.py:723-749) on the fly
-            i32 pa = B.a.best_p, qa = B.a.best_q, pb = B.b.best_p, qb = B.b.best_q;
-            abort_any |= (pa == -1) || (pb == -1);
-            if (base + k == 0) {
-                if (pa == -1) { pa = old_last_ba; qa = 0; }
-                if (pb == -1) { pb = old_last_bb; qb = 0; }
-            }
-            if (pa == -1) qa = 0;
-            if (pb == -1) qb = 0;
-            if (pa != -1) prev_a = pa;
-            if (pb != -1) prev_b = pb;
-            cap = wlane(cap, prev_a, k); caq = wlane(caq, qa, k);
-            cbp = wlane(cbp, prev_b, k); cbq = wlane(cbq, qb, k);
+            rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
+            rpb = wlane(rpb, B.b.best_p, k); rqb = wlane(rqb, B.b.best_q, k);
         }
+        // abort flag on raw quotes; _ffill_best_prices (marl_env.py:723-749) for the chunk
+        abort_any |= bal((l < cnt) & ((rpa == -1) | (rpb == -1))) != 0ull;
+        i32 pa = rpa, pb = rpb;
+        if ((base == 0) & (l == 0)) {
+            pa = pa == -1 ? old_last_ba : pa;
+            pb = pb == -1 ? old_last_bb : pb;
+        }
+        const i32 caq = rpa == -1 ? 0 : rqa, cbq = rpb == -1 ? 0 : rqb;
+        const i32 cap = ffill(pa, prev_a), cbp = ffill(pb, prev_b);
+        prev_a = rdl(cap, cnt - 1);
+        prev_b = rdl(cbp, cnt - 1);
         if (row < M) {
             reinterpret_cast<int2*>(rec + c.off_best_asks)[row] = make_int2(cap, caq);
             reinterpret_cast<int2*>(rec + c.off_best_bids)[row] = make_int2(cbp, cbq);
