@@ -73,14 +73,10 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from hftlob import dist as D
+    R = D.init_from_env("nccl")
+    world, rank, local = R.world, R.rank, R.local
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from hftlob.config_io import builtin_config
     from hftlob.data.synthetic import generate_day
@@ -95,8 +91,7 @@ def main():
         d = generate_day(n_msgs=args.n_msgs, mid=args.mid, snap_every=snap)
         np.savez(cache + ".tmp.npz", msgs=d.msgs, books=d.books, snap_idx=d.snap_idx, tick=d.tick_size)
         os.replace(cache + ".tmp.npz", cache)
-    if dist is not None:
-        dist.barrier()
+    D.barrier(R)
     from hftlob.data.synthetic import LobsterDay
     z = np.load(cache)
     day = LobsterDay(msgs=z["msgs"], books=z["books"], snap_idx=z["snap_idx"], tick_size=int(z["tick"]))
@@ -107,7 +102,7 @@ def main():
     # global key split, then this rank's slice (reference pmap layout: contiguous env blocks)
     master = torch.tensor([[0, 0]], dtype=torch.int32, device="cuda")
     all_keys = split_keys(master, world * E + 1)[0]
-    keys0 = all_keys[1 + rank * E: 1 + (rank + 1) * E].contiguous()
+    keys0 = D.rank_keys(all_keys, rank, E).contiguous()
     _, state = env.reset(keys0, params)
     rng = torch.tensor([[0, 1 + rank]], dtype=torch.int32, device="cuda")
 
@@ -125,28 +120,21 @@ def main():
     for _ in range(args.warmup):
         rng = one_step(rng)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    D.barrier(R)
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    D.barrier(R)
     t0 = time.perf_counter()
     for k in range(args.steps):
         rng = one_step(rng, events[k])
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    D.barrier(R)
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = D.max_over_ranks(R, elapsed, device="cuda")
 
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        D.finalize(R)
         return
     value = world * E * args.steps / elapsed
     per_env = algorithmic_bytes_per_env_step(env)
@@ -184,8 +172,7 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    D.finalize(R)
 
 
 if __name__ == "__main__":

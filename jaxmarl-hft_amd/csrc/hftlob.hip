@@ -332,21 +332,18 @@ template <int S> DEV void clear_masked(i32* t, int R, const lmask (&m)[S]) {
     lds_order();
 }
 
-// _removeZeroNegQuant — JaxOrderBookArrays.py:85-90, after row e was written
-// with quantity qe.  Clean side: only row e can hold q <= 0.
-template <int S> DEV void rzn(Side<S>& s, int R, const Valid<S>& V, int e, i32 qe) {
-    if (s.clean) {
-        if (qe <= 0) clr6(s.t, s.scr, R, e);
-    } else {
-        i32 q[S];
-        ldcol(s.t, R, FQ, q);
-        lmask m[S];
+// _removeZeroNegQuant — JaxOrderBookArrays.py:85-90 on a side that is not
+// clean (on a clean side only the row just written can hold q <= 0, and the
+// handlers clear it directly)
+template <int S> DEV void rzn(Side<S>& s, int R, const Valid<S>& V) {
+    i32 q[S];
+    ldcol(s.t, R, FQ, q);
+    lmask m[S];
 #pragma unroll
-        for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
-        clear_masked(s.t, R, m);
-        s.clean = true;
-        s.ok = false;
-    }
+    for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
+    clear_masked(s.t, R, m);
+    s.clean = true;
+    s.ok = false;
 }
 
 // get_best_bid: max raw price (empty side -> -1); volume at it — :943-951,906-917
@@ -473,12 +470,16 @@ DEV void trade_put(Trades& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32
 }
 
 // ------------------------------------------------------ message handlers
+// G (general) = false instantiates the handlers for the common case where
+// both sides are clean and neg1-free (flags that only add_order can change):
+// the kernels run that variant while B.fast holds.
 template <int S>
 struct Book {
     Side<S> a, b;
     Trades tr;
     Valid<S> vs, vt;
     LobCfg c;
+    bool fast;  // a.clean & b.clean & !a.neg1 & !b.neg1
 };
 
 struct Msg {
@@ -512,7 +513,7 @@ template <int S> DEV void note_reduce(Side<S>& s, i32 op, i32 dq) {
 }
 
 // match_order — JaxOrderBookArrays.py:172-220
-template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
+template <bool G, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
     const int R = B.c.nO;
     const i32 qt = ldu(s.t, R, FQ, top), pt = ldu(s.t, R, FP, top);
     const i32 ot = ldu(s.t, R, FOID, top), tt = ldu(s.t, R, FTID, top);
@@ -523,13 +524,13 @@ template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, c
     for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(B.tr.get(4, r) == -1);  // trade[:,OID=4] == -1
     const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
-    if (s.clean) {
+    if (!G || s.clean) {
         if (newq <= 0) clr6(s.t, s.scr, R, top);
         else stu(s.t, s.scr, R, FQ, top, newq);
         note_reduce(s, pt, wsub(qt, newq));
     } else {
         stu(s.t, s.scr, R, FQ, top, newq);
-        rzn(s, R, B.vs, top, newq);
+        rzn(s, R, B.vs);
     }
     return rem;
 }
@@ -537,7 +538,7 @@ template <int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, c
 // _match_against_{bid,ask}_orders — :284-331.  The top slot's price never
 // beats the side's best, so "best does not cross" ends the loop exactly; only
 // a crossing best pays for the 3-reduction top-of-book.
-template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
+template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     while (qtm > 0) {
         if (!s.ok) { if (BID) best_bid(s, B.c.nO, B.vs); else best_ask(s, B.c.nO, B.vs, B.c.maxint); }
         const i32 mp = BID ? s.best_p : (s.best_p == -1 ? B.c.maxint : s.best_p);
@@ -545,18 +546,18 @@ template <bool BID, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm
         const int top = top_idx(s, B.vs, B.c, mp);
         const i32 tp = ldu(s.t, B.c.nO, FP, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
-        qtm = match_order(B, s, top, qtm, m);
+        qtm = match_order<G>(B, s, top, qtm, m);
     }
     return qtm;
 }
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
-template <bool BID, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
+template <bool BID, bool G, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
     const int R = B.c.nO;
     lmask fm[S];
     i32 p[S];
     ldcol(s.t, R, FP, p);
-    const bool fast = s.clean && !s.neg1;  // then "any -1" <=> p == -1
+    const bool fast = !G || (s.clean && !s.neg1);  // then "any -1" <=> p == -1
     if (fast) {
 #pragma unroll
         for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == -1);
@@ -571,16 +572,19 @@ template <bool BID, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg&
     }
     const int e = first_slot(fm, R - 1);
     const i32 nq = imax_(0, qty);
-    if (!s.clean) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
+    if (G && !s.clean) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
         st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        rzn(s, R, B.vs, e, nq);
+        rzn(s, R, B.vs);
         return;
     }
     const i32 op = sget(p, e), oq = ldu(s.t, R, FQ, e);
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
         st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1))) s.neg1 = true;
+        if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1))) {
+            s.neg1 = true;
+            B.fast = false;
+        }
         if (was_empty) note_add<BID>(s, m.price, nq, B.c.maxint);
         else s.ok = false;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
@@ -611,21 +615,21 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
 }
 
 // bid_lim — :357-420 (discard: a type-4 message under type_4_interpretation 0/2)
-template <int S> DEV void bid_lim(Book<S>& B, Msg m, bool discard) {
-    const i32 rem = match_against<false>(B, B.a, m.qty, m.price, m);
+template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m, bool discard) {
+    const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
     if (B.c.check_fill) evict_if_full<true>(B, B.b);
-    if (!discard) add_order<true>(B, B.b, m, rem);
+    if (!discard) add_order<true, G>(B, B.b, m, rem);
 }
 // ask_lim — :446-508
-template <int S> DEV void ask_lim(Book<S>& B, Msg m, bool discard) {
+template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m, bool discard) {
     if (B.c.t4 == 2) m.price = 0;
-    const i32 rem = match_against<true>(B, B.b, m.qty, m.price, m);
+    const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
     if (B.c.check_fill) evict_if_full<false>(B, B.a);
-    if (!discard) add_order<false>(B, B.a, m, rem);
+    if (!discard) add_order<false, G>(B, B.a, m, rem);
 }
 // cancel_order + get_init_id_match — :93-139
-template <int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+template <bool G, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     const int R = B.c.nO;
     i32 o[S];
     ldcol(s.t, R, FOID, o);
@@ -646,13 +650,13 @@ template <int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     }
     const i32 op = ldu(s.t, R, FP, idx), oq = ldu(s.t, R, FQ, idx);
     const i32 nq = wsub(oq, m.qty);
-    if (s.clean) {
+    if (!G || s.clean) {
         if (nq <= 0) clr6(s.t, s.scr, R, idx);
         else stu(s.t, s.scr, R, FQ, idx, nq);
         note_reduce(s, op, wsub(oq, nq > 0 ? nq : 0));
     } else {
         stu(s.t, s.scr, R, FQ, idx, nq);
-        rzn(s, R, B.vs, idx, nq);
+        rzn(s, R, B.vs);
     }
 }
 
@@ -674,15 +678,20 @@ DEV void decode_msgs(const LobCfg& c, int4& x) {
     x.x = h;
     x.y = sd;
 }
-template <int S> DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+template <bool G, int S>
+DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
     m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
     const i32 kind = h & H_KIND;
     const bool disc = (h & H_DISCARD) != 0;
-    if (kind == H_CNL_ASK) cancel(B, B.a, m);
-    else if (kind == H_CNL_BID) cancel(B, B.b, m);
-    else if (kind == H_BID) bid_lim(B, m, disc);
-    else if (kind == H_ASK) ask_lim(B, m, disc);
+    if (kind == H_CNL_ASK) cancel<G>(B, B.a, m);
+    else if (kind == H_CNL_BID) cancel<G>(B, B.b, m);
+    else if (kind == H_BID) bid_lim<G>(B, m, disc);
+    else if (kind == H_ASK) ask_lim<G>(B, m, disc);
+}
+template <int S> DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+    if (B.fast) process_msg_<false>(B, h, d1, d2, d3, d4, d5, d6, d7);
+    else process_msg_<true>(B, h, d1, d2, d3, d4, d5, d6, d7);
 }
 // forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
 DEV i32 ffill(i32 v, i32 carry) {
@@ -731,6 +740,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     load_side(B.a, ga, R, B.vs);
     load_side(B.b, gb, R, B.vs);
     load_trades(B.tr, gt, B.vt);
+    B.fast = B.a.clean & B.b.clean & !B.a.neg1 & !B.b.neg1;
     const i32* gm = msgs + (size_t)e * n_msg * 8;
     for (int base = 0; base < n_msg; base += 64) {
         const int row = base + l;
@@ -1480,6 +1490,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     }
     load_side(B.a, rec + c.off_asks, R, B.vs);
     load_side(B.b, rec + c.off_bids, R, B.vs);
+    B.fast = B.a.clean & B.b.clean & !B.a.neg1 & !B.b.neg1;
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
     {

@@ -307,6 +307,7 @@ class MARLEnv:
                                               _lib.ptr(params.loaded_params.message_data),
                                               _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf),
                                               C.byref(o["struct"]), _lib.stream_ptr()))
+        self.last_info_words = o["info"]  # raw info record of the last step (int32 [E, info_words]) or None
         obs = self._split_types(o["obs"], True)
         rewards = self._split_types(o["rewards"], False)
         dones = {"__all__": o["done_all"].bool(), "agents": [d.bool() for d in self._split_types(o["dones"], False)]}

@@ -1,0 +1,108 @@
+"""The C-ABI library without a GPU: it loads, exports every entry point that
+include/hftlob.h declares, agrees with the host's ctypes structs on sizes and
+offsets, and rejects bad calls with the documented codes before any device
+work (hftlob.h: HFTLOB_ENULL / EINVAL / ESHAPE)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from hftlob import _lib
+from hftlob.config_io import builtin_config
+from hftlob.layout import AgentTypeCfg, EnvCfg, LobCfg, StepOut, pack_env_cfg, pack_lob_cfg
+from oracle import pyoracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hftlob.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(hftlob_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_exports():
+    assert _declared() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libhftlob.so not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    missing = [s for s in _declared() if s not in syms]
+    assert not missing, missing
+    L = _lib.lib()                                   # loads, checks the ABI version
+    assert L.hftlob_version() == _lib.ABI_VERSION
+
+
+def test_struct_layout_matches_c():
+    lay = O.abi_layout()
+    assert lay[0] == C.sizeof(LobCfg)
+    assert lay[1] == C.sizeof(AgentTypeCfg)
+    assert lay[2] == C.sizeof(EnvCfg)
+    assert lay[3] == EnvCfg.types.offset
+    assert lay[4] == AgentTypeCfg.rebate_factor.offset
+    assert lay[5] == C.sizeof(StepOut)
+    assert lay[6] == EnvCfg.info_words.offset
+    assert lay[7] == AgentTypeCfg.task.offset
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libhftlob.so not built")
+    return _lib.lib()
+
+
+def _env_cfg(name="2_player_fq_fqc"):
+    c, _ = pack_env_cfg(builtin_config(name), 10, 100_000, True)
+    return c
+
+
+def test_error_null_and_shape(L):
+    assert L.hftlob_book_process(None, 1, 1, None, None, None, None, None, None, None) == -2
+    lob = pack_lob_cfg(builtin_config("2_player_fq_fqc").world_config)
+    assert L.hftlob_book_process(C.byref(lob), -1, 1, None, None, None, None, None, None, None) == -3
+    assert L.hftlob_book_process(C.byref(lob), 0, 1, None, None, None, None, None, None, None) == 0  # empty batch
+    assert L.hftlob_book_process(C.byref(lob), 4, 8, None, None, None, None, None, None, None) == -2
+    assert b"null" in L.hftlob_last_error()
+    c = _env_cfg()
+    out = StepOut()
+    assert L.hftlob_env_step(C.byref(c), 4, None, None, None, None, None, C.byref(out), None) == -2
+    assert L.hftlob_env_reset(None, 4, None, None, None, None, None, None) == -2
+    assert L.hftlob_split_keys(4, 0, 1, None, None, None) == -3
+    assert L.hftlob_sample_actions(None, 4, None, None, None) == -2
+
+
+@pytest.mark.parametrize("field,value,code", [("cancel_mode", 2, -1), ("type_4_interpretation", 3, -1),
+                                              ("n_orders", 0, -3), ("n_trades", 257, -3)])
+def test_error_bad_lob_cfg(L, field, value, code):
+    lob = pack_lob_cfg(builtin_config("2_player_fq_fqc").world_config)
+    setattr(lob, field, value)
+    dummy = C.c_void_p(16)  # never dereferenced: validation fails first
+    assert L.hftlob_book_process(C.byref(lob), 1, 1, dummy, dummy, dummy, dummy, None, None, None) == code
+
+
+def test_error_bad_env_cfg(L):
+    dummy = C.c_void_p(16)
+    out = StepOut(16, 16, 16, 16, None)
+    for mutate, code in ((lambda c: setattr(c, "ep_type", 1), -1),
+                         (lambda c: setattr(c, "n_agents", 3), -1),
+                         (lambda c: setattr(c, "n_msgs", 1000), -3),
+                         (lambda c: setattr(c.types[0], "kind", 7), -1),
+                         (lambda c: setattr(c.types[0], "sell_buy_all_option", 1), -1)):
+        c = _env_cfg()
+        mutate(c)
+        rc = L.hftlob_env_step(C.byref(c), 1, dummy, dummy, dummy, dummy, dummy, C.byref(out), None)
+        assert rc == code, (rc, code)
+
+
+def test_device_tensors_required():
+    import torch
+    with pytest.raises(RuntimeError, match="device"):
+        _lib.ptr(torch.zeros(4, dtype=torch.int32))

@@ -1,4 +1,10 @@
-"""Fused env step parity: HIP hftlob_env_step vs the CPU oracle over episodes."""
+"""Fused env step parity: HIP hftlob_env_step vs the CPU oracle over episodes.
+
+Integer words of the state record (book, trades, best arrays, ids, counters)
+must be bit-exact; float words, obs and rewards within rtol = atol = 1e-5.
+"""
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -9,6 +15,8 @@ from hftlob.env import MARLEnv, split_keys
 from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
+
+RTOL = ATOL = 1e-5
 
 
 def _float_words(env):
@@ -26,18 +34,45 @@ def _compare_state(env, o, g, tag):
     bad = np.argwhere((o != g) & mask[None, :])
     assert bad.size == 0, f"{tag}: int word mismatch (env, word) {bad[:5].tolist()} oracle {o[tuple(bad[0])]} gpu {g[tuple(bad[0])]}"
     of, gf = o[:, fw].view(np.float32), g[:, fw].view(np.float32)
-    assert np.allclose(of, gf, rtol=1e-5, atol=1e-5, equal_nan=True), f"{tag}: float words differ"
+    assert np.allclose(of, gf, rtol=RTOL, atol=RTOL, equal_nan=True), f"{tag}: float words differ"
 
 
-@pytest.mark.parametrize("name,mid", [("2_player_fq_fqc", 2_000_000), ("2_player_fq_fqc", 28_000_000),
-                                      ("mm_debug_fixed_quant", 2_000_000)])
-def test_env_rollout_parity(name, mid):
-    cfg = builtin_config(name)
+def _compare_info(env, o, g, tag):
+    from hftlob.layout import AGENT_MM, INFO_AGENT_WORDS, INFO_EXE, INFO_MM, INFO_WORLD, INFO_WORLD_WORDS
+    isf = np.zeros(o.shape[1], bool)
+    for k, (_, f) in enumerate(INFO_WORLD):
+        isf[k] = f
+    for a, kind in enumerate(env.layout.agent_kinds):
+        for k, (_, f) in enumerate(INFO_MM if kind == AGENT_MM else INFO_EXE):
+            isf[INFO_WORLD_WORDS + a * INFO_AGENT_WORDS + k] = f
+    bad = np.argwhere((o != g) & ~isf[None, :])
+    assert bad.size == 0, f"{tag}: info int word mismatch {bad[:5].tolist()}"
+    assert np.allclose(o[:, isf].view(np.float32), g[:, isf].view(np.float32), rtol=RTOL, atol=ATOL,
+                       equal_nan=True), f"{tag}: info float words differ"
+
+
+def variant(cfg, type_name, **changes):
+    """A copy of `cfg` with fields of one agent type replaced (configs are frozen dataclasses)."""
+    agents = dict(cfg.dict_of_agents_configs)
+    agents[type_name] = dataclasses.replace(agents[type_name], **changes)
+    return dataclasses.replace(cfg, dict_of_agents_configs=agents)
+
+
+_DAYS = {}
+
+
+def _day(w, mid, seed=11):
+    key = (mid, seed, w.n_data_msg_per_step * w.start_resolution)
+    if key not in _DAYS:
+        _DAYS[key] = generate_day(n_msgs=30_000, seed=seed, mid=mid, snap_every=key[2])
+    return _DAYS[key]
+
+
+def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11):
     w = cfg.world_config
-    day = generate_day(n_msgs=30_000, seed=11, mid=mid, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    day = _day(w, mid, seed)
     env = MARLEnv(None, cfg, data=day)
     params = env.default_params
-    E, K = 64, 70                                         # crosses the 64-step episode end (auto-reset)
     init = O.init_states(env.cfg_c.lob, env.windows, day.msgs, w, env.layout.init_rec_words)
     assert (init == env._init_states.cpu().numpy()).all()
     keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
@@ -46,7 +81,7 @@ def test_env_rollout_parity(name, mid):
     _compare_state(env, o_state, state.buf.cpu().numpy(), "reset")
     assert np.allclose(torch.cat([x.reshape(E, -1) for x in obs], 1).cpu().numpy(),
                        np.concatenate([o_obs[:, i, :d] for i, d in enumerate(
-                           [env.layout.obs_dims[t] for t in env.layout.agent_types])], 1), rtol=1e-5, atol=1e-6)
+                           [env.layout.obs_dims[t] for t in env.layout.agent_types])], 1), rtol=RTOL, atol=1e-6)
     rng = keys
     for k in range(K):
         nk = split_keys(rng, 2)
@@ -60,10 +95,49 @@ def test_env_rollout_parity(name, mid):
                                                   init, prev)
         _compare_state(env, st, state.buf.cpu().numpy(), f"step {k}")
         g_rew = torch.cat([x.reshape(E, -1) for x in rew], 1).cpu().numpy()
-        assert np.allclose(g_rew, orw, rtol=1e-5, atol=1e-5), f"step {k}: rewards"
+        assert np.allclose(g_rew, orw, rtol=RTOL, atol=ATOL), f"step {k}: rewards"
         assert (dones["__all__"].cpu().numpy() == oda.astype(bool)).all()
         a0 = 0
         for t, n in enumerate(cfg.number_of_agents_per_type):
             d = env.layout.obs_dims[t]
-            assert np.allclose(obs[t].cpu().numpy(), oo[:, a0:a0 + n, :d], rtol=1e-5, atol=1e-6), f"step {k}: obs type {t}"
+            assert np.allclose(obs[t].cpu().numpy(), oo[:, a0:a0 + n, :d], rtol=RTOL, atol=1e-6), f"step {k}: obs type {t}"
+            g_dn = dones["agents"][t].cpu().numpy()
+            assert (g_dn == odn[:, a0:a0 + n].astype(bool)).all(), f"step {k}: dones type {t}"
             a0 += n
+        _compare_info(env, oinfo, env.last_info_words.cpu().numpy(), f"step {k}")
+
+
+@pytest.mark.parametrize("name,mid", [("2_player_fq_fqc", 2_000_000), ("2_player_fq_fqc", 28_000_000),
+                                      ("mm_debug_fixed_quant", 2_000_000),
+                                      ("3_player_fq_fqc_dir", 2_000_000),
+                                      ("exec_debug_fixed_quants_complex", 2_000_000)])
+def test_env_rollout_parity(name, mid):
+    rollout_parity(builtin_config(name), mid)
+
+
+MM_VARIANTS = [
+    dict(reward_function=r) for r in ("portfolio_value", "buy_sell_pnl", "complex", "zero_inv", "spooner",
+                                      "spooner_damped", "spooner_asym_damped", "spooner_scaled",
+                                      "delta_portfolio_value")
+] + [
+    dict(reference_price="mid_avg", unwind_price="mid_avg"),
+    dict(reference_price="far_touch", unwind_price="far_touch"),
+    dict(reference_price="near_touch", inv_penalty="linear"),
+    dict(inv_penalty="quadratic", clip_reward=True),
+    dict(inv_penalty="threshold", exclude_extreme_spreads=True, volume_traded_bonus="market_share"),
+    dict(auto_liquidate_threshold=3, normalize=False),
+]
+
+
+@pytest.mark.parametrize("changes", MM_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+def test_mm_option_parity(changes):
+    rollout_parity(variant(builtin_config("2_player_fq_fqc"), "MarketMaking", **changes), E=32, K=66)
+
+
+EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid", task="buy"),
+                dict(task="sell", normalize=False)]
+
+
+@pytest.mark.parametrize("changes", EXE_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+def test_exe_option_parity(changes):
+    rollout_parity(variant(builtin_config("2_player_fq_fqc"), "Execution", **changes), E=32, K=66)
