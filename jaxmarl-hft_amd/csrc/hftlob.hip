@@ -271,17 +271,29 @@ template <int S>
 struct Side {
     i32* t;              // LDS table [6][R]
     i32* scr;            // LDS scratch row (64 words)
-    // wave-uniform bookkeeping (SGPRs)
-    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid when ok
-    bool ok;             // cache valid
-    bool clean;          // every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
-                         // ever has to look at the row just written
-    bool neg1;           // some row with p != -1 holds a -1 in another field (then "first row
-                         // holding ANY -1" needs the full test, else p == -1 suffices)
+    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid under F_OK
 };
 
-// global [R][6] rows -> LDS side table, with the clean / neg1 flags
-template <int S> DEV void load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
+// Wave-uniform book flags, one SGPR bitfield (bools would each be a 64-bit
+// lane mask the compiler copies at every merge):
+//   OK     the side's cached best quote is valid
+//   CLEAN  every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
+//          ever has to look at the row just written
+//   NEG1   some row with p != -1 holds a -1 in another field (then "first row
+//          holding ANY -1" needs the full test, else p == -1 suffices)
+//   FAST   both sides CLEAN and neither NEG1 (the handlers' common variant)
+enum : u32 { F_OK_A = 1, F_OK_B = 2, F_CLEAN_A = 4, F_CLEAN_B = 8, F_NEG1_A = 16, F_NEG1_B = 32, F_FAST = 64 };
+template <bool ASKS> struct SideBits {
+    static constexpr u32 OK = ASKS ? F_OK_A : F_OK_B;
+    static constexpr u32 CLEAN = ASKS ? F_CLEAN_A : F_CLEAN_B;
+    static constexpr u32 NEG1 = ASKS ? F_NEG1_A : F_NEG1_B;
+};
+DEV u32 fast_bit(u32 fl) {
+    return (fl & (F_CLEAN_A | F_CLEAN_B | F_NEG1_A | F_NEG1_B)) == (F_CLEAN_A | F_CLEAN_B) ? F_FAST : 0u;
+}
+
+// global [R][6] rows -> LDS side table; returns the side's CLEAN / NEG1 bits
+template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
     const int l = lane_id();
     lmask bad = 0, n1 = 0;
 #pragma unroll
@@ -301,9 +313,7 @@ template <int S> DEV void load_side(Side<S>& s, const i32* g, int R, const Valid
         n1 |= V.m[r] & ~bal(p == -1) & any;
     }
     lds_order();
-    s.clean = bad == 0ull;
-    s.neg1 = n1 != 0ull;
-    s.ok = false;
+    return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u);
 }
 template <int S> DEV void store_side(const Side<S>& s, i32* g, int R, const Valid<S>& V) {
     const int l = lane_id();
@@ -335,15 +345,15 @@ template <int S> DEV void clear_masked(i32* t, int R, const lmask (&m)[S]) {
 // _removeZeroNegQuant — JaxOrderBookArrays.py:85-90 on a side that is not
 // clean (on a clean side only the row just written can hold q <= 0, and the
 // handlers clear it directly)
-template <int S> DEV void rzn(Side<S>& s, int R, const Valid<S>& V) {
+template <bool ASKS, int S> DEV void rzn(Side<S>& s, u32& fl, int R, const Valid<S>& V) {
     i32 q[S];
     ldcol(s.t, R, FQ, q);
     lmask m[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
     clear_masked(s.t, R, m);
-    s.clean = true;
-    s.ok = false;
+    fl = (fl | SideBits<ASKS>::CLEAN) & ~SideBits<ASKS>::OK;
+    fl = (fl & ~F_FAST) | fast_bit(fl);
 }
 
 // get_best_bid: max raw price (empty side -> -1); volume at it — :943-951,906-917
@@ -372,19 +382,14 @@ DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i3
     bp = pa;
     bq = wave_sum(v);
 }
-template <int S> DEV void best_bid(Side<S>& s, int R, const Valid<S>& V) {
+// recompute a side's cached best quote (sets its OK bit)
+template <bool ASKS, int S> DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint) {
     i32 p[S], q[S];
     ldcol(s.t, R, FP, p);
     ldcol(s.t, R, FQ, q);
-    best_bid_pq(p, q, V, s.best_p, s.best_q);
-    s.ok = true;
-}
-template <int S> DEV void best_ask(Side<S>& s, int R, const Valid<S>& V, i32 maxint) {
-    i32 p[S], q[S];
-    ldcol(s.t, R, FP, p);
-    ldcol(s.t, R, FQ, q);
-    best_ask_pq(p, q, V, maxint, s.best_p, s.best_q);
-    s.ok = true;
+    if (ASKS) best_ask_pq(p, q, V, maxint, s.best_p, s.best_q);
+    else best_bid_pq(p, q, V, s.best_p, s.best_q);
+    fl |= SideBits<ASKS>::OK;
 }
 
 // _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
@@ -472,14 +477,14 @@ DEV void trade_put(Trades& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32
 // ------------------------------------------------------ message handlers
 // G (general) = false instantiates the handlers for the common case where
 // both sides are clean and neg1-free (flags that only add_order can change):
-// the kernels run that variant while B.fast holds.
+// the kernels run that variant while F_FAST is set.
 template <int S>
 struct Book {
     Side<S> a, b;
     Trades tr;
     Valid<S> vs, vt;
     LobCfg c;
-    bool fast;  // a.clean & b.clean & !a.neg1 & !b.neg1
+    u32 fl;  // F_* bits
 };
 
 struct Msg {
@@ -489,31 +494,33 @@ struct Msg {
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
 // side: it changes (best_p, best_q) only where get_best_* / get_volume_at_price
 // would, and falls back to a full recompute (ok = false) where it cannot tell.
-template <bool BID, int S> DEV void note_add(Side<S>& s, i32 np, i32 nq, i32 maxint) {
+template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq, i32 maxint) {
     // an all -1 row now holds (np, nq > 0)
-    if (!s.ok) return;
+    constexpr u32 OK = SideBits<!BID>::OK;
+    if (!(fl & OK)) return;
     if (BID) {
         if (s.best_p == -1) {
-            if (np > -1) { s.best_p = np; s.best_q = nq; } else s.ok = false;
+            if (np > -1) { s.best_p = np; s.best_q = nq; } else fl &= ~OK;
         } else if (np > s.best_p) { s.best_p = np; s.best_q = nq; }
         else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
     } else {
-        if (np == -1 || np == maxint) { if (s.best_p == -1) s.ok = false; return; }
+        if (np == -1 || np == maxint) { if (s.best_p == -1) fl &= ~OK; return; }
         if (s.best_p == -1 || np < s.best_p) { s.best_p = np; s.best_q = nq; }
         else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
     }
 }
 // a row at price op lost dq of its quantity (possibly all of it)
-template <int S> DEV void note_reduce(Side<S>& s, i32 op, i32 dq) {
-    if (!s.ok) return;
-    if (op == -1 || s.best_p == -1) { s.ok = false; return; }
+template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i32 dq) {
+    constexpr u32 OK = SideBits<ASKS>::OK;
+    if (!(fl & OK)) return;
+    if (op == -1 || s.best_p == -1) { fl &= ~OK; return; }
     if (op != s.best_p) return;
     s.best_q = wsub(s.best_q, dq);
-    if (s.best_q <= 0) s.ok = false;  // level exhausted (or odd data): rescan
+    if (s.best_q <= 0) fl &= ~OK;  // level exhausted (or odd data): rescan
 }
 
 // match_order — JaxOrderBookArrays.py:172-220
-template <bool G, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
+template <bool G, bool ASKS, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
     const int R = B.c.nO;
     const i32 qt = ldu(s.t, R, FQ, top), pt = ldu(s.t, R, FP, top);
     const i32 ot = ldu(s.t, R, FOID, top), tt = ldu(s.t, R, FTID, top);
@@ -524,13 +531,13 @@ template <bool G, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i3
     for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(B.tr.get(4, r) == -1);  // trade[:,OID=4] == -1
     const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
-    if (!G || s.clean) {
+    if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (newq <= 0) clr6(s.t, s.scr, R, top);
         else stu(s.t, s.scr, R, FQ, top, newq);
-        note_reduce(s, pt, wsub(qt, newq));
+        note_reduce<ASKS>(s, B.fl, pt, wsub(qt, newq));
     } else {
         stu(s.t, s.scr, R, FQ, top, newq);
-        rzn(s, R, B.vs);
+        rzn<ASKS>(s, B.fl, R, B.vs);
     }
     return rem;
 }
@@ -540,13 +547,13 @@ template <bool G, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i3
 // a crossing best pays for the 3-reduction top-of-book.
 template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     while (qtm > 0) {
-        if (!s.ok) { if (BID) best_bid(s, B.c.nO, B.vs); else best_ask(s, B.c.nO, B.vs, B.c.maxint); }
+        if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, B.c.nO, B.vs, B.c.maxint);
         const i32 mp = BID ? s.best_p : (s.best_p == -1 ? B.c.maxint : s.best_p);
         if (BID ? !(mp >= price) : !(mp <= price)) break;
         const int top = top_idx(s, B.vs, B.c, mp);
         const i32 tp = ldu(s.t, B.c.nO, FP, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
-        qtm = match_order<G>(B, s, top, qtm, m);
+        qtm = match_order<G, !BID>(B, s, top, qtm, m);
     }
     return qtm;
 }
@@ -557,7 +564,8 @@ template <bool BID, bool G, int S> DEV void add_order(Book<S>& B, Side<S>& s, co
     lmask fm[S];
     i32 p[S];
     ldcol(s.t, R, FP, p);
-    const bool fast = !G || (s.clean && !s.neg1);  // then "any -1" <=> p == -1
+    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK;
+    const bool fast = !G || ((B.fl & (CLEAN | NEG1)) == CLEAN);  // then "any -1" <=> p == -1
     if (fast) {
 #pragma unroll
         for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == -1);
@@ -572,24 +580,22 @@ template <bool BID, bool G, int S> DEV void add_order(Book<S>& B, Side<S>& s, co
     }
     const int e = first_slot(fm, R - 1);
     const i32 nq = imax_(0, qty);
-    if (G && !s.clean) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
+    if (G && !(B.fl & CLEAN)) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
         st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        rzn(s, R, B.vs);
+        rzn<!BID>(s, B.fl, R, B.vs);
         return;
     }
     const i32 op = sget(p, e), oq = ldu(s.t, R, FQ, e);
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
         st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1))) {
-            s.neg1 = true;
-            B.fast = false;
-        }
-        if (was_empty) note_add<BID>(s, m.price, nq, B.c.maxint);
-        else s.ok = false;
+        if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1)))
+            B.fl = (B.fl | NEG1) & ~F_FAST;
+        if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
+        else B.fl &= ~OK;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         clr6(s.t, s.scr, R, e);
-        s.ok = false;
+        B.fl &= ~OK;
     }
 }
 
@@ -611,7 +617,7 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(p[r] == worst);
     clear_masked(s.t, R, m);
-    s.ok = false;
+    B.fl &= ~SideBits<!BID>::OK;
 }
 
 // bid_lim — :357-420 (discard: a type-4 message under type_4_interpretation 0/2)
@@ -629,7 +635,7 @@ template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m, bool discard) {
     if (!discard) add_order<false, G>(B, B.a, m, rem);
 }
 // cancel_order + get_init_id_match — :93-139
-template <bool G, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     const int R = B.c.nO;
     i32 o[S];
     ldcol(s.t, R, FOID, o);
@@ -650,13 +656,13 @@ template <bool G, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     }
     const i32 op = ldu(s.t, R, FP, idx), oq = ldu(s.t, R, FQ, idx);
     const i32 nq = wsub(oq, m.qty);
-    if (!G || s.clean) {
+    if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (nq <= 0) clr6(s.t, s.scr, R, idx);
         else stu(s.t, s.scr, R, FQ, idx, nq);
-        note_reduce(s, op, wsub(oq, nq > 0 ? nq : 0));
+        note_reduce<ASKS>(s, B.fl, op, wsub(oq, nq > 0 ? nq : 0));
     } else {
         stu(s.t, s.scr, R, FQ, idx, nq);
-        rzn(s, R, B.vs);
+        rzn<ASKS>(s, B.fl, R, B.vs);
     }
 }
 
@@ -684,13 +690,13 @@ DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5,
     m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
     const i32 kind = h & H_KIND;
     const bool disc = (h & H_DISCARD) != 0;
-    if (kind == H_CNL_ASK) cancel<G>(B, B.a, m);
-    else if (kind == H_CNL_BID) cancel<G>(B, B.b, m);
+    if (kind == H_CNL_ASK) cancel<G, true>(B, B.a, m);
+    else if (kind == H_CNL_BID) cancel<G, false>(B, B.b, m);
     else if (kind == H_BID) bid_lim<G>(B, m, disc);
     else if (kind == H_ASK) ask_lim<G>(B, m, disc);
 }
 template <int S> DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
-    if (B.fast) process_msg_<false>(B, h, d1, d2, d3, d4, d5, d6, d7);
+    if (B.fl & F_FAST) process_msg_<false>(B, h, d1, d2, d3, d4, d5, d6, d7);
     else process_msg_<true>(B, h, d1, d2, d3, d4, d5, d6, d7);
 }
 // forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
@@ -702,8 +708,10 @@ DEV i32 ffill(i32 v, i32 carry) {
     return src < 0 ? carry : got;
 }
 template <int S> DEV void refresh_best(Book<S>& B) {
-    if (!B.a.ok) best_ask(B.a, B.c.nO, B.vs, B.c.maxint);
-    if (!B.b.ok) best_bid(B.b, B.c.nO, B.vs);
+    if ((B.fl & (F_OK_A | F_OK_B)) != (F_OK_A | F_OK_B)) {
+        if (!(B.fl & F_OK_A)) rescan<true>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint);
+        if (!(B.fl & F_OK_B)) rescan<false>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint);
+    }
 }
 
 // LDS carve-up of one env's book: [asks 6*nO][bids 6*nO][trades 8*nT][pad 64*4]
@@ -737,10 +745,9 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     i32* ga = asks + (size_t)e * R * 6;
     i32* gb = bids + (size_t)e * R * 6;
     i32* gt = trades + (size_t)e * B.c.nT * 8;
-    load_side(B.a, ga, R, B.vs);
-    load_side(B.b, gb, R, B.vs);
+    B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs);
+    B.fl |= fast_bit(B.fl);
     load_trades(B.tr, gt, B.vt);
-    B.fast = B.a.clean & B.b.clean & !B.a.neg1 & !B.b.neg1;
     const i32* gm = msgs + (size_t)e * n_msg * 8;
     for (int base = 0; base < n_msg; base += 64) {
         const int row = base + l;
@@ -1488,9 +1495,8 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             excl_any = ballot(any) != 0ull;
         }
     }
-    load_side(B.a, rec + c.off_asks, R, B.vs);
-    load_side(B.b, rec + c.off_bids, R, B.vs);
-    B.fast = B.a.clean & B.b.clean & !B.a.neg1 & !B.b.neg1;
+    B.fl = load_side<true>(B.a, rec + c.off_asks, R, B.vs) | load_side<false>(B.b, rec + c.off_bids, R, B.vs);
+    B.fl |= fast_bit(B.fl);
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
     {

@@ -76,7 +76,7 @@ def run():
 
 
 def report(d):
-    rows = list(csv.DictReader(open(os.path.join(d, "pmc_counter_collection.csv"))))
+    rows = list(csv.DictReader(open(os.path.join(d, "mc_counter_collection.csv"))))
     disp = collections.OrderedDict()
     for r in rows:
         if "k_book_process" in r["Kernel_Name"] and int(r["Grid_Size"]) == E * 64:
