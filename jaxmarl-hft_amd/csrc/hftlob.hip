@@ -246,12 +246,19 @@ DEV void clr6(i32* t, i32* scr, int R, int e) {
     *(l < 6 ? t + l * R + e : scr + l) = -1;
     lds_order();
 }
-// first slot over per-register lane masks; `fallback` if none
+// s_ff1_i32_b64: index of the lowest set bit, -1 (all ones) for an empty mask
+DEV u32 ff1(lmask m) {
+    u32 r;
+    asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    return r;
+}
+// first slot over per-register lane masks; `fallback` if none.  An empty
+// register's -1 survives `| 64*r` and loses every unsigned min.
 template <int S> DEV int first_slot(const lmask (&m)[S], int fallback) {
-    int idx = fallback;
+    u32 idx = ff1(m[0]);
 #pragma unroll
-    for (int r = S - 1; r >= 0; --r) idx = m[r] ? r * 64 + ffs64(m[r]) : idx;
-    return idx;
+    for (int r = 1; r < S; ++r) idx = min(idx, ff1(m[r]) | (u32)(64 * r));
+    return idx == 0xFFFFFFFFu ? fallback : (int)idx;
 }
 template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
     lmask m[S];
@@ -487,8 +494,10 @@ struct Book {
     u32 fl;  // F_* bits
 };
 
+// message handler codes (the reference's dispatch index) and flags, see decode_msgs
+enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8, H_NEG1 = 16 };
 struct Msg {
-    i32 side, price, qty, oid, tid, t, tns;
+    i32 h, side, price, qty, oid, tid, t, tns;  // h: handler code and H_* flags (decode_msgs)
 };
 
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
@@ -559,11 +568,11 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
 }
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
-template <bool BID, bool G, int S> DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty) {
+// p: the side's price column (already loaded by the caller)
+template <bool BID, bool G, int S>
+DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)[S]) {
     const int R = B.c.nO;
     lmask fm[S];
-    i32 p[S];
-    ldcol(s.t, R, FP, p);
     constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK;
     const bool fast = !G || ((B.fl & (CLEAN | NEG1)) == CLEAN);  // then "any -1" <=> p == -1
     if (fast) {
@@ -589,8 +598,7 @@ template <bool BID, bool G, int S> DEV void add_order(Book<S>& B, Side<S>& s, co
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
         st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        if ((m.price != -1) & ((m.oid == -1) | (m.tid == -1) | (m.t == -1) | (m.tns == -1)))
-            B.fl = (B.fl | NEG1) & ~F_FAST;
+        if (m.h & H_NEG1) B.fl = (B.fl | NEG1) & ~F_FAST;
         if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
         else B.fl &= ~OK;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
@@ -599,11 +607,10 @@ template <bool BID, bool G, int S> DEV void add_order(Book<S>& B, Side<S>& s, co
     }
 }
 
-// check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max)
-template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
+// check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max);
+// p is the side's price column, reloaded here if rows were cleared
+template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&p)[S]) {
     const int R = B.c.nO;
-    i32 p[S];
-    ldcol(s.t, R, FP, p);
     lmask neg = 0;
 #pragma unroll
     for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(p[r] < 0);
@@ -618,21 +625,26 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s) {
     for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(p[r] == worst);
     clear_masked(s.t, R, m);
     B.fl &= ~SideBits<!BID>::OK;
+    ldcol(s.t, R, FP, p);
 }
 
-// bid_lim — :357-420 (discard: a type-4 message under type_4_interpretation 0/2)
-template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m, bool discard) {
+// bid_lim — :357-420 (the eviction persists when the add is discarded)
+template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
-    if (B.c.check_fill) evict_if_full<true>(B, B.b);
-    if (!discard) add_order<true, G>(B, B.b, m, rem);
+    i32 p[S];
+    ldcol(B.b.t, B.c.nO, FP, p);
+    if (B.c.check_fill) evict_if_full<true>(B, B.b, p);
+    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, p);
 }
 // ask_lim — :446-508
-template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m, bool discard) {
+template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (B.c.t4 == 2) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
-    if (B.c.check_fill) evict_if_full<false>(B, B.a);
-    if (!discard) add_order<false, G>(B, B.a, m, rem);
+    i32 p[S];
+    ldcol(B.a.t, B.c.nO, FP, p);
+    if (B.c.check_fill) evict_if_full<false>(B, B.a, p);
+    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p);
 }
 // cancel_order + get_init_id_match — :93-139
 template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
@@ -670,9 +682,12 @@ template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, cons
 //   1 side==1 & type in {1,4}; 2 side==-1 & type in {2,3}; 3 side==1 & type in {2,3};
 //   4 side==0 & type==0 (doNothing); everything else 0 (ask_lim); side flipped for type 4.
 // Evaluated in VALU for the 64 messages of a chunk at once (lane = message):
-// x = (type, side, qty, price) becomes (handler | H_DISCARD, side', qty, price).
-enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8 };
-DEV void decode_msgs(const LobCfg& c, int4& x) {
+// x = (type, side, qty, price) becomes (handler | flags, side', qty, price).
+// H_DISCARD: a type-4 message under type_4_interpretation 0/2 is not added
+// after matching.  H_NEG1: the row add_order would write has p != -1 and a -1
+// in another field (it sets the side's NEG1 flag); the price it writes is the
+// message's, or maxint / 0 for MKT bids / asks.
+DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     const i32 ty = x.x, sd = ty == 4 ? wsub(0, x.y) : x.y;
     const bool cnl = (ty == 2) | (ty == 3);
     i32 h = H_ASK;
@@ -681,19 +696,20 @@ DEV void decode_msgs(const LobCfg& c, int4& x) {
     h = (cnl & (sd == 1)) ? H_CNL_BID : h;
     h = (cnl & (sd == -1)) ? H_CNL_ASK : h;
     if (((c.t4 == 0) | (c.t4 == 2)) & (ty == 4)) h |= H_DISCARD;
+    const i32 p_add = c.t4 == 2 ? (h == H_BID ? c.maxint : 0) : x.w;
+    if ((p_add != -1) & ((y.x == -1) | (y.y == -1) | (y.z == -1) | (y.w == -1))) h |= H_NEG1;
     x.x = h;
     x.y = sd;
 }
 template <bool G, int S>
 DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
-    m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
+    m.h = h; m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
     const i32 kind = h & H_KIND;
-    const bool disc = (h & H_DISCARD) != 0;
     if (kind == H_CNL_ASK) cancel<G, true>(B, B.a, m);
     else if (kind == H_CNL_BID) cancel<G, false>(B, B.b, m);
-    else if (kind == H_BID) bid_lim<G>(B, m, disc);
-    else if (kind == H_ASK) ask_lim<G>(B, m, disc);
+    else if (kind == H_BID) bid_lim<G>(B, m);
+    else if (kind == H_ASK) ask_lim<G>(B, m);
 }
 template <int S> DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     if (B.fl & F_FAST) process_msg_<false>(B, h, d1, d2, d3, d4, d5, d6, d7);
@@ -756,7 +772,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
             x = reinterpret_cast<const int4*>(gm + row * 8)[0];
             y = reinterpret_cast<const int4*>(gm + row * 8)[1];
         }
-        decode_msgs(B.c, x);
+        decode_msgs(B.c, x, y);
         i32 ap = 0, aq = 0, bp = 0, bq = 0;
         const int cnt = imin_(64, n_msg - base);
         for (int k = 0; k < cnt; ++k) {
@@ -1589,7 +1605,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             x = reinterpret_cast<const int4*>(g)[0];
             y = reinterpret_cast<const int4*>(g)[1];
         }
-        decode_msgs(B.c, x);
+        decode_msgs(B.c, x, y);
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
         const int cnt = imin_(64, M - base);
         for (int k = 0; k < cnt; ++k) {

@@ -76,17 +76,24 @@ def run():
 
 
 def report(d):
-    rows = list(csv.DictReader(open(os.path.join(d, "mc_counter_collection.csv"))))
+    import glob
     disp = collections.OrderedDict()
-    for r in rows:
-        if "k_book_process" in r["Kernel_Name"] and int(r["Grid_Size"]) == E * 64:
-            disp.setdefault(int(r["Dispatch_Id"]), {})[r["Counter_Name"]] = float(r["Counter_Value"])
-    ids = sorted(disp)[-len(KINDS):]
-    names = sorted({k for v in disp.values() for k in v})
-    print("per message per wave:", " ".join(n.replace("SQ_", "") for n in names))
-    for kind, i in zip(KINDS, ids):
-        v = disp[i]
-        print(f"{kind:18s}", " ".join(f"{v[n] / E / N:9.1f}" for n in names))
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
+        rows = [r for r in csv.DictReader(open(f))
+                if "k_book_process" in r["Kernel_Name"] and int(r["Grid_Size"]) == E * 64]
+        ids = sorted({int(r["Dispatch_Id"]) for r in rows})[-len(KINDS):]
+        for r in rows:
+            i = int(r["Dispatch_Id"])
+            if i in ids:
+                disp.setdefault(KINDS[ids.index(i)], {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    names = sorted({k for v in disp.values() for k in v} - {"SQ_WAVES"})
+    short = [n.replace("SQ_", "").replace("INSTS_", "I_").replace("ACTIVE_INST_", "A_").replace("ICACHE_", "IC_")
+             for n in names]
+    print("per message per wave (cycle counters in quad-cycles; SQC_* per message per CU-pair estimate):")
+    print(f"{'':18s}" + "".join(f"{s:>10s}" for s in short))
+    for kind in KINDS:
+        v = disp.get(kind, {})
+        print(f"{kind:18s}" + "".join(f"{v.get(n, float('nan')) / E / N:10.1f}" for n in names))
 
 
 if __name__ == "__main__":
