@@ -266,11 +266,12 @@ template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
     for (int r = 0; r < S; ++r) m[r] = bal(pr[r]);
     return first_slot(m, fallback);
 }
+// value of (uniform) slot e from a column held lane-strided in registers
 template <int S> DEV i32 sget(const i32 (&a)[S], int e) {
-    i32 v = 0;
+    const int l = e & 63;
+    i32 v = rdl(a[0], l);
 #pragma unroll
-    for (int k = 0; k < S; ++k)
-        if (S == 1 || (e >> 6) == k) v = rdl(a[k], e & 63);
+    for (int k = 1; k < S; ++k) v = (e >> 6) == k ? rdl(a[k], l) : v;
     return v;
 }
 
@@ -401,12 +402,9 @@ template <bool ASKS, int S> DEV void rescan(Side<S>& s, u32& fl, int R, const Va
 
 // _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
 // mp is the side's max price (bid) / min price with -1 -> maxint (ask)
-template <int S> DEV int top_idx(const Side<S>& s, const Valid<S>& V, const LobCfg& c, i32 mp) {
-    const int R = c.nO;
-    i32 p[S], ts[S], tns[S], t[S], n[S], m = INT_MAX;
-    ldcol(s.t, R, FP, p);
-    ldcol(s.t, R, FTS, ts);
-    ldcol(s.t, R, FTNS, tns);
+template <int S>
+DEV int top_idx(const i32 (&p)[S], const i32 (&ts)[S], const i32 (&tns)[S], const Valid<S>& V, const LobCfg& c, i32 mp) {
+    i32 t[S], n[S], m = INT_MAX;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         t[r] = (p[r] == mp) ? ts[r] : c.maxint;
@@ -529,15 +527,17 @@ template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i3
 }
 
 // match_order — JaxOrderBookArrays.py:172-220
-template <bool G, bool ASKS, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m) {
+// (qt, pt, ot, tt): the top slot's quantity, price, order id, trader id;
+// tr4: the trade log's OID column
+template <bool G, bool ASKS, int S>
+DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 qt, i32 pt, i32 ot, i32 tt,
+                    const i32 (&tr4)[S]) {
     const int R = B.c.nO;
-    const i32 qt = ldu(s.t, R, FQ, top), pt = ldu(s.t, R, FP, top);
-    const i32 ot = ldu(s.t, R, FOID, top), tt = ldu(s.t, R, FTID, top);
     const i32 newq = imax_(0, wsub(qt, qtm));
     const i32 rem = wsub(qtm, qt);
     lmask fm[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(B.tr.get(4, r) == -1);  // trade[:,OID=4] == -1
+    for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(tr4[r] == -1);  // trade[:,OID=4] == -1
     const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
@@ -554,23 +554,29 @@ template <bool G, bool ASKS, int S> DEV i32 match_order(Book<S>& B, Side<S>& s, 
 // _match_against_{bid,ask}_orders — :284-331.  The top slot's price never
 // beats the side's best, so "best does not cross" ends the loop exactly; only
 // a crossing best pays for the 3-reduction top-of-book.
+// a crossing trip loads every column it needs at once (one LDS round trip)
 template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
+    const int R = B.c.nO;
     while (qtm > 0) {
-        if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, B.c.nO, B.vs, B.c.maxint);
+        if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
         const i32 mp = BID ? s.best_p : (s.best_p == -1 ? B.c.maxint : s.best_p);
         if (BID ? !(mp >= price) : !(mp <= price)) break;
-        const int top = top_idx(s, B.vs, B.c, mp);
-        const i32 tp = ldu(s.t, B.c.nO, FP, top);
+        i32 p[S], q[S], o[S], t[S], ts[S], tn[S], tr4[S];
+        ldcol(s.t, R, FP, p); ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
+        ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
+        ldcol(B.tr.t, B.tr.R, 4, tr4);
+        const int top = top_idx(p, ts, tn, B.vs, B.c, mp);
+        const i32 tp = sget(p, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
-        qtm = match_order<G, !BID>(B, s, top, qtm, m);
+        qtm = match_order<G, !BID>(B, s, top, qtm, m, sget(q, top), tp, sget(o, top), sget(t, top), tr4);
     }
     return qtm;
 }
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
-// p: the side's price column (already loaded by the caller)
+// p, q: the side's price and quantity columns (loaded by the caller)
 template <bool BID, bool G, int S>
-DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)[S]) {
+DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)[S], const i32 (&q)[S]) {
     const int R = B.c.nO;
     lmask fm[S];
     constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK;
@@ -579,8 +585,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)
 #pragma unroll
         for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == -1);
     } else {
-        i32 q[S], o[S], t[S], ts[S], tn[S];
-        ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
+        i32 o[S], t[S], ts[S], tn[S];
+        ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
         ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
 #pragma unroll
         for (int r = 0; r < S; ++r)
@@ -594,7 +600,7 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)
         rzn<!BID>(s, B.fl, R, B.vs);
         return;
     }
-    const i32 op = sget(p, e), oq = ldu(s.t, R, FQ, e);
+    const i32 op = sget(p, e), oq = sget(q, e);
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
         st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
@@ -609,7 +615,7 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)
 
 // check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max);
 // p is the side's price column, reloaded here if rows were cleared
-template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&p)[S]) {
+template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&p)[S], i32 (&q)[S]) {
     const int R = B.c.nO;
     lmask neg = 0;
 #pragma unroll
@@ -626,39 +632,41 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&
     clear_masked(s.t, R, m);
     B.fl &= ~SideBits<!BID>::OK;
     ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FQ, q);
 }
 
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
-    i32 p[S];
+    i32 p[S], q[S];
     ldcol(B.b.t, B.c.nO, FP, p);
-    if (B.c.check_fill) evict_if_full<true>(B, B.b, p);
-    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, p);
+    ldcol(B.b.t, B.c.nO, FQ, q);
+    if (B.c.check_fill) evict_if_full<true>(B, B.b, p, q);
+    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, p, q);
 }
 // ask_lim — :446-508
 template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (B.c.t4 == 2) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
-    i32 p[S];
+    i32 p[S], q[S];
     ldcol(B.a.t, B.c.nO, FP, p);
-    if (B.c.check_fill) evict_if_full<false>(B, B.a, p);
-    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p);
+    ldcol(B.a.t, B.c.nO, FQ, q);
+    if (B.c.check_fill) evict_if_full<false>(B, B.a, p, q);
+    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p, q);
 }
 // cancel_order + get_init_id_match — :93-139
 template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     const int R = B.c.nO;
-    i32 o[S];
+    i32 o[S], p[S], q[S];
     ldcol(s.t, R, FOID, o);
+    ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FQ, q);
     lmask fm[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
     int idx = first_slot(fm, -1);
     if (idx < 0) {
-        i32 p[S], q[S];
-        ldcol(s.t, R, FP, p);
-        ldcol(s.t, R, FQ, q);
         const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
 #pragma unroll
         for (int r = 0; r < S; ++r)
@@ -666,7 +674,7 @@ template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, cons
                     bal(q[r] >= m.qty);
         idx = first_slot(fm, R - 1);  // -1 wraps to the last slot
     }
-    const i32 op = ldu(s.t, R, FP, idx), oq = ldu(s.t, R, FQ, idx);
+    const i32 op = sget(p, idx), oq = sget(q, idx);
     const i32 nq = wsub(oq, m.qty);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (nq <= 0) clr6(s.t, s.scr, R, idx);
