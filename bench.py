@@ -3,8 +3,11 @@
 (gymnax_exchange/jaxen/Speed_test.py:140-224):
 
   per step:  rng, *step_keys = split(rng, NUM_ENVS + 1)
-             actions = per-type randint from split(step_key, n_types)   (device)
-             env.step(step_key, state, actions, params)                  (one fused HIP launch)
+             actions = per-type randint from split(step_key, n_types)
+             env.step(step_key, state, actions, params)
+  all three in ONE HIP launch (MARLEnv.step_sampled -> hftlob_env_step_sampled);
+  the unfused three-launch form is checked bit-exact against it in
+  tests/test_gpu_env.py.
 
 Weak scaling: every rank (one process per GPU) steps its own 4096 envs on a
 replicated synthetic LOBSTER day; no collective on the data path (only the
@@ -104,21 +107,20 @@ def main():
     all_keys = split_keys(master, world * E + 1)[0]
     keys0 = D.rank_keys(all_keys, rank, E).contiguous()
     _, state = env.reset(keys0, params)
-    rng = torch.tensor([[0, 1 + rank]], dtype=torch.int32, device="cuda")
+    kbuf = [torch.tensor([0, 1 + rank], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
+    nstep = [0]
 
-    def one_step(rng, ev=None):
-        ks = split_keys(rng, E + 1)[0]
-        rng, step_keys = ks[0:1].contiguous(), ks[1:].contiguous()
-        acts = env.sample_actions(step_keys)
+    def one_step(ev=None):
+        k = nstep[0]
         if ev is not None:
             ev[0].record()
-        env.step(step_keys, state, acts, params)
+        env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)
         if ev is not None:
             ev[1].record()
-        return rng
+        nstep[0] = k + 1
 
     for _ in range(args.warmup):
-        rng = one_step(rng)
+        one_step()
     torch.cuda.synchronize()
     D.barrier(R)
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -126,7 +128,7 @@ def main():
     D.barrier(R)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        rng = one_step(rng, events[k])
+        one_step(events[k])
     torch.cuda.synchronize()
     D.barrier(R)
     elapsed = time.perf_counter() - t0
@@ -148,8 +150,10 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         n_env_cpu, n_steps_cpu = 4096, 64       # one full episode (incl. auto-reset) of the metric workload
         v, thr = cpu_baseline(env, day, n_env_cpu, n_steps_cpu, args.cpu_threads)
+        v1, _ = cpu_baseline(env, day, 512, 16, 1)
         cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": thr, "kind": "port",
-               "sample": f"{n_env_cpu} envs x {n_steps_cpu} steps of the same config/day, C oracle (OpenMP)"}
+               "sample": f"{n_env_cpu} envs x {n_steps_cpu} steps of the same config/day, C oracle (OpenMP)",
+               "single_core_value": round(v1, 1), "single_core_sample": "512 envs x 16 steps, 1 thread"}
     line = {
         "metric": "env steps/sec (whole node), 2-agent MARL, 10-level LOB, NUM_ENVS=4096",
         "value": round(value, 1),

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HFTLOB_ABI_VERSION 1
+#define HFTLOB_ABI_VERSION 2
 
 #define HFTLOB_OK            0
 #define HFTLOB_EINVAL      (-1)   /* bad config value / unsupported option */
@@ -183,16 +183,16 @@ typedef struct hftlob_env_cfg {
  * info may be NULL (skipped).  Layouts:
  *   obs      f32   [n_env][n_agents][obs_stride]   (agent order = type order)
  *   rewards  f32   [n_env][n_agents]
- *   done_all int32 [n_env]                         dones["__all__"]
- *   dones    int32 [n_env][n_agents]               dones["agents"]
+ *   done_all bool (uint8 0/1) [n_env]              dones["__all__"]
+ *   dones    bool (uint8 0/1) [n_env][n_agents]    dones["agents"]
  *   info     32-bit words [n_env][info_words]: world info then one
  *            HFTLOB_INFO_AGENT_WORDS block per agent (ints, or f32 bit-cast;
  *            field map in hftlob/layout.py) */
 typedef struct hftlob_step_out {
     float*   obs;
     float*   rewards;
-    int32_t* done_all;
-    int32_t* dones;
+    uint8_t* done_all;
+    uint8_t* dones;
     int32_t* info;
 } hftlob_step_out;
 
@@ -200,6 +200,9 @@ int         hftlob_version(void);
 const char* hftlob_last_error(void);
 
 /* Batched order-book message processing (engine operator).
+ * Replaces jax.vmap(scan_through_entire_array_save_bidask) —
+ * gymnax_exchange/jaxob/JaxOrderBookArrays.py:791-823 — and, with NULL best
+ * arrays, jax.vmap(scan_through_entire_array) — :736-756.
  * msgs      [n_env][n_msg][8]      message rows [type,side,q,p,oid,tid,s,ns]
  * asks,bids [n_env][n_orders][6]   in/out
  * trades    [n_env][n_trades][8]   in/out (caller initialises, e.g. all -1)
@@ -209,24 +212,43 @@ int hftlob_book_process(const hftlob_lob_cfg* cfg /*[host]*/, int n_env, int n_m
                         const int32_t* msgs, int32_t* asks, int32_t* bids, int32_t* trades,
                         int32_t* best_asks, int32_t* best_bids, void* stream);
 
-/* Batched MARLEnv.reset.  keys uint32 [n_env][2]; state [n_env][rec_words].
+/* Batched MARLEnv.reset — replaces jax.vmap(env.reset, (0, None)):
+ * gymnax_exchange/jaxen/marl_env.py:763-770 (reset_env :129-207,
+ * BaseLOBEnv.reset_env base_env.py:218-234).
+ * keys uint32 [n_env][2]; state [n_env][rec_words].
  * msg_data [n_data_rows][8]; init_states [n_windows][init_rec_words]. */
 int hftlob_env_reset(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint32_t* keys,
                      const int32_t* msg_data, const int32_t* init_states,
                      int32_t* state, const hftlob_step_out* out /*[host] struct*/, void* stream);
 
-/* Batched MARLEnv.step with auto-reset.  actions int32 [n_env][n_agents]. */
+/* Batched MARLEnv.step with auto-reset — replaces
+ * jax.vmap(env.step, in_axes=(0, 0, 0, None)): marl_env.py:775-804 (step_env
+ * :211-709).  keys uint32 [n_env][2]; actions int32 [n_env][n_agents]. */
 int hftlob_env_step(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint32_t* keys,
                     const int32_t* actions, const int32_t* msg_data, const int32_t* init_states,
                     int32_t* state, const hftlob_step_out* out /*[host] struct*/, void* stream);
 
-/* Speed_test action sampling: for env e with step key k_e,
+/* One Speed_test rollout step in a single launch — replaces the body of
+ * _env_step in gymnax_exchange/jaxen/Speed_test.py:165-185:
+ *   rng, *step_keys = split(rng, n_env + 1)      (key_in -> key_out, step keys)
+ *   actions = hftlob_sample_actions(step_keys)     (written to actions_out if not NULL)
+ *   hftlob_env_step(step_keys, actions, ...)
+ * key_in / key_out: uint32 [2] device buffers, distinct (every env reads
+ * key_in; key_out receives split(key_in, n_env + 1)[0]). */
+int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint32_t* key_in,
+                            uint32_t* key_out, int32_t* actions_out, const int32_t* msg_data,
+                            const int32_t* init_states, int32_t* state, const hftlob_step_out* out /*[host] struct*/,
+                            void* stream);
+
+/* Speed_test action sampling (Speed_test.py:166-177, gymnax Discrete.sample):
+ * for env e with step key k_e,
  * sub = split(k_e, n_types); per type t, agent i:
  * actions[e][agent] = randint(split(sub[t], n_agents_t)[i], 0, n_actions_t). */
 int hftlob_sample_actions(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint32_t* keys,
                           int32_t* actions, void* stream);
 
-/* Batched jax.random.split: out[e][j] = split(keys[e], n)[j]; out [n_env][n][2]. */
+/* Batched jax.random.split (threefry2x32; partitionable = jax_threefry_partitionable):
+ * out[e][j] = split(keys[e], n)[j]; out [n_env][n][2]. */
 int hftlob_split_keys(int n_env, int n, int partitionable, const uint32_t* keys,
                       uint32_t* out, void* stream);
 

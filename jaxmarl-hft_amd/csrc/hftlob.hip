@@ -26,6 +26,7 @@
 
 typedef int32_t i32;
 typedef uint32_t u32;
+typedef uint8_t u8;
 #define DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------- wave utils
@@ -1476,11 +1477,16 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
 template <int S, int NFIX>
+// master != NULL: Speed_test rollout mode — the env's step key is
+// split(master, n_env + 1)[e + 1], actions are sampled here (hftlob_sample_actions)
+// and written to actions_io if it is not NULL; env 0 writes split(master)[0]
+// to master_out.  Otherwise keys / actions_io are the inputs.
 __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
-                                                 const i32* __restrict__ actions, const i32* __restrict__ msg_data,
+                                                 const u32* __restrict__ master, u32* __restrict__ master_out,
+                                                 i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
                                                  const i32* __restrict__ init_states, i32* __restrict__ state,
                                                  float* __restrict__ obs_out, float* __restrict__ rew_out,
-                                                 i32* __restrict__ done_all_out, i32* __restrict__ dones_out,
+                                                 u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
                                                  i32* __restrict__ info_out) {
     extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
@@ -1498,7 +1504,18 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     if (NFIX > 0) { B.c.nO = NFIX; B.c.nT = NFIX; }
     const int R = B.c.nO;
     book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
-    const Key key{keys[2 * e], keys[2 * e + 1]};
+    Key key;
+    if (master) {
+        const Key mk{master[0], master[1]};
+        key = split_key(mk, n_env + 1, e + 1, part);
+        if ((e == 0) & (l == 0)) {
+            const Key k0 = split_key(mk, n_env + 1, 0, part);
+            master_out[0] = k0.a;
+            master_out[1] = k0.b;
+        }
+    } else {
+        key = Key{keys[2 * e], keys[2 * e + 1]};
+    }
     const Key k1 = split_key(key, 2, 0, part), key_reset = split_key(key, 2, 1, part);
     // loaded / world scalars (wave-uniform)
     const i32* Lr = rec + c.off_loaded;
@@ -1530,7 +1547,14 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             const hftlob_agent_type_cfg& tc = c.types[t];
             for (int i = 0; i < tc.n_agents; ++i, ++ag) {
                 const i32 tid = wsub(tc.trader_id0, i);
-                const i32 act = actions[(size_t)e * c.n_agents + ag];
+                i32 act;
+                if (master) {  // Speed_test.py:166-177 (as k_sample_actions)
+                    const Key sub = split_key(key, c.n_types, t, part);
+                    act = randint(split_key(sub, tc.n_agents, i, part), 0, tc.n_actions, part);
+                    if (actions_io && l == 0) actions_io[(size_t)e * c.n_agents + ag] = act;
+                } else {
+                    act = actions_io[(size_t)e * c.n_agents + ag];
+                }
                 i32 s4[4] = {st[0], st[1], st[2], st[3]};
                 ActX x{0, 0, 0, 0, 0, 0};
                 if (tc.kind == HFTLOB_AGENT_MM) {
@@ -1723,7 +1747,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                 }
                 if (l == 0) {
                     rew_out[(size_t)e * c.n_agents + ag] = rew;
-                    dones_out[(size_t)e * c.n_agents + ag] = d;
+                    dones_out[(size_t)e * c.n_agents + ag] = (u8)(d != 0);
                 }
                 if (info) {
                     i32 v = 0;
@@ -1753,7 +1777,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         for (int k = 0; k < HFTLOB_INFO_WORLD_WORDS; ++k) if (l == k) v = wv_[k];
         if (l < HFTLOB_INFO_WORLD_WORDS) info[l] = v;
     }
-    if (l == 0) done_all_out[e] = all;
+    if (l == 0) done_all_out[e] = (u8)all;
 #ifdef HFTLOB_STAMPS
     if (info && l == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
@@ -1886,6 +1910,26 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
     return launch_status();
 }
 
+static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const uint32_t* key_in,
+                           uint32_t* key_out, int32_t* actions, const int32_t* msg_data, const int32_t* init_states,
+                           int32_t* state, const hftlob_step_out* out, void* stream) {
+    if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
+    const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(n_env), b(64);
+    const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
+                            12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+#define LAUNCH_STEP(SS, NF) hipLaunchKernelGGL((k_env_step<SS, NF>), g, b, shm, st, *cfg, n_env, keys, key_in, key_out, \
+                                               actions, msg_data, init_states, state, out->obs, out->rewards, \
+                                               out->done_all, out->dones, out->info)
+    if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100);
+    else if (S == 1) LAUNCH_STEP(1, 0);
+    else if (S == 2) LAUNCH_STEP(2, 0);
+    else LAUNCH_STEP(4, 0);
+#undef LAUNCH_STEP
+    return launch_status();
+}
+
 int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const int32_t* actions,
                     const int32_t* msg_data, const int32_t* init_states, int32_t* state, const hftlob_step_out* out,
                     void* stream) {
@@ -1894,21 +1938,21 @@ int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, 
     if (n_env < 0) return fail(HFTLOB_ESHAPE, "negative n_env");
     if (n_env == 0) return HFTLOB_OK;
     if (!keys || !actions || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
-    if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
-    const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
-    hipStream_t st = (hipStream_t)stream;
-    dim3 g(n_env), b(64);
-    const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
-                            12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
-#define LAUNCH_STEP(SS, NF) hipLaunchKernelGGL((k_env_step<SS, NF>), g, b, shm, st, *cfg, n_env, keys, actions, msg_data, \
-                                               init_states, state, out->obs, out->rewards, out->done_all, out->dones, \
-                                               out->info)
-    if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100);
-    else if (S == 1) LAUNCH_STEP(1, 0);
-    else if (S == 2) LAUNCH_STEP(2, 0);
-    else LAUNCH_STEP(4, 0);
-#undef LAUNCH_STEP
-    return launch_status();
+    return env_step_launch(cfg, n_env, keys, nullptr, nullptr, const_cast<int32_t*>(actions), msg_data, init_states,
+                           state, out, stream);
+}
+
+int hftlob_env_step_sampled(const hftlob_env_cfg* cfg, int n_env, const uint32_t* key_in, uint32_t* key_out,
+                            int32_t* actions_out, const int32_t* msg_data, const int32_t* init_states,
+                            int32_t* state, const hftlob_step_out* out, void* stream) {
+    int rc = check_env(cfg);
+    if (rc) return rc;
+    if (n_env < 0) return fail(HFTLOB_ESHAPE, "negative n_env");
+    if (n_env == 0) return HFTLOB_OK;
+    if (!key_in || !key_out || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
+    if (key_in == key_out) return fail(HFTLOB_EINVAL, "key_in and key_out must be distinct buffers");
+    return env_step_launch(cfg, n_env, nullptr, key_in, key_out, actions_out, msg_data, init_states, state, out,
+                           stream);
 }
 
 int hftlob_sample_actions(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, int32_t* actions, void* stream) {

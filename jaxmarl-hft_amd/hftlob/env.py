@@ -222,8 +222,8 @@ class MARLEnv:
         L, dev = self.layout, self.device
         o = {"obs": torch.empty((E, self.num_agents, L.obs_stride), dtype=torch.float32, device=dev),
              "rewards": torch.empty((E, self.num_agents), dtype=torch.float32, device=dev),
-             "done_all": torch.empty((E,), dtype=torch.int32, device=dev),
-             "dones": torch.empty((E, self.num_agents), dtype=torch.int32, device=dev),
+             "done_all": torch.empty((E,), dtype=torch.bool, device=dev),
+             "dones": torch.empty((E, self.num_agents), dtype=torch.bool, device=dev),
              "info": torch.empty((E, L.info_words), dtype=torch.int32, device=dev) if self.return_info else None}
         o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
                               _lib.ptr(o["dones"]), _lib.ptr(o["info"]) if o["info"] is not None else None)
@@ -307,10 +307,30 @@ class MARLEnv:
                                               _lib.ptr(params.loaded_params.message_data),
                                               _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf),
                                               C.byref(o["struct"]), _lib.stream_ptr()))
+        return self._results(o, state, E)
+
+    def step_sampled(self, key_in: torch.Tensor, key_out: torch.Tensor, state: MultiAgentState,
+                     params: MultiAgentParams, actions_out: Optional[torch.Tensor] = None):
+        """One Speed_test rollout step (Speed_test.py:165-185) in one launch:
+        ``key_out, *step_keys = split(key_in, E + 1)``, per-type randint actions
+        from the step keys (written to ``actions_out`` [E, num_agents] if given),
+        then ``step``.  key_in / key_out: distinct uint32 [2] device tensors."""
+        E = state.buf.shape[0]
+        o = self._outputs(E)
+        if actions_out is not None and (tuple(actions_out.shape) != (E, self.num_agents)
+                                        or actions_out.dtype != torch.int32):
+            raise ValueError("actions_out must be int32 [E, num_agents]")
+        _lib.check(_lib.lib().hftlob_env_step_sampled(
+            C.byref(self.cfg_c), E, _lib.ptr(key_in), _lib.ptr(key_out), _lib.ptr(actions_out),
+            _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
+            _lib.ptr(state.buf), C.byref(o["struct"]), _lib.stream_ptr()))
+        return self._results(o, state, E)
+
+    def _results(self, o, state, E):
         self.last_info_words = o["info"]  # raw info record of the last step (int32 [E, info_words]) or None
         obs = self._split_types(o["obs"], True)
         rewards = self._split_types(o["rewards"], False)
-        dones = {"__all__": o["done_all"].bool(), "agents": [d.bool() for d in self._split_types(o["dones"], False)]}
+        dones = {"__all__": o["done_all"], "agents": self._split_types(o["dones"], False)}
         return obs, state, rewards, dones, self._info(o, E)
 
     def sample_actions(self, key: torch.Tensor) -> torch.Tensor:

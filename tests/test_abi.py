@@ -76,6 +76,9 @@ def test_error_null_and_shape(L):
     assert L.hftlob_env_step(C.byref(c), 4, None, None, None, None, None, C.byref(out), None) == -2
     assert L.hftlob_env_reset(None, 4, None, None, None, None, None, None) == -2
     assert L.hftlob_split_keys(4, 0, 1, None, None, None) == -3
+    k = C.c_void_p(64)
+    assert L.hftlob_env_step_sampled(C.byref(c), 4, k, None, None, k, k, k, C.byref(out), None) == -2
+    assert L.hftlob_env_step_sampled(C.byref(c), 4, k, k, None, k, k, k, C.byref(out), None) == -1  # key_in == key_out
     assert L.hftlob_sample_actions(None, 4, None, None, None) == -2
 
 

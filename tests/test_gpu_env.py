@@ -141,3 +141,32 @@ EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid",
 @pytest.mark.parametrize("changes", EXE_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
 def test_exe_option_parity(changes):
     rollout_parity(variant(builtin_config("2_player_fq_fqc"), "Execution", **changes), E=32, K=66)
+
+
+def test_step_sampled_equals_split_sample_step():
+    """hftlob_env_step_sampled (one launch) == split_keys + sample_actions + env_step."""
+    cfg = builtin_config("2_player_fq_fqc")
+    w = cfg.world_config
+    env = MARLEnv(None, cfg, data=_day(w, 2_000_000))
+    params = env.default_params
+    E = 48
+    keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
+    _, s1 = env.reset(keys, params)
+    s2 = s1.clone(env)
+    kbuf = [torch.tensor([0, 7], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
+    rng = kbuf[0].clone().reshape(1, 2)
+    acts_out = torch.empty((E, env.num_agents), dtype=torch.int32, device="cuda")
+    for k in range(70):
+        o1, s1, r1, d1, _ = env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], s1, params, acts_out)
+        o1 = [x.clone() for x in o1]
+        r1 = [x.clone() for x in r1]
+        da1 = d1["__all__"].clone()
+        ks = split_keys(rng, E + 1)[0]
+        rng, sk = ks[0:1].contiguous(), ks[1:].contiguous()
+        acts = env.sample_actions(sk)
+        o2, s2, r2, d2, _ = env.step(sk, s2, acts, params)
+        assert (acts_out == acts).all(), f"step {k}: sampled actions"
+        assert (kbuf[(k + 1) % 2] == rng[0]).all(), f"step {k}: carried key"
+        assert (s1.buf == s2.buf).all(), f"step {k}: state"
+        assert all((a == b).all() for a, b in zip(o1, o2)) and all((a == b).all() for a, b in zip(r1, r2))
+        assert (da1 == d2["__all__"]).all()

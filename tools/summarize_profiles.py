@@ -1,0 +1,47 @@
+"""Summarise a tools/profile_round.sh directory: kernel stats, HBM traffic per
+k_env_step launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), SQ counters
+per wave.  Writes <dir>/pmc_traffic.json and prints a text summary."""
+import csv
+import glob
+import json
+import os
+import sys
+
+d = sys.argv[1]
+
+
+def rows(sub, pat="*counter_collection.csv"):
+    f = glob.glob(os.path.join(d, sub, "**", pat), recursive=True)
+    return list(csv.DictReader(open(f[0]))) if f else []
+
+
+def per_launch(sub, counter, kernel="k_env_step"):
+    vals = [float(r["Counter_Value"]) for r in rows(sub) if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    return sum(vals) / len(vals) if vals else None
+
+
+stats = glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursive=True)
+if stats:
+    print("== rocprofv3 --kernel-trace --stats (bench.py --no-cpu-baseline)")
+    for r in csv.DictReader(open(stats[0])):
+        print(f"{r['Name'][:60]:60s} calls {r['Calls']:>6s} avg_ns {float(r['AverageNs']):12.1f} "
+              f"total_pct {float(r['Percentage']):6.2f}")
+fetch_kb, write_kb = per_launch("fetch", "FETCH_SIZE"), per_launch("write", "WRITE_SIZE")
+bench = json.load(open(os.path.join(d, "stats_bench.json"))) if os.path.exists(os.path.join(d, "stats_bench.json")) else {}
+E = bench.get("config", {}).get("num_envs_per_gpu", 4096)
+out = {}
+if fetch_kb is not None and write_kb is not None:
+    hbm = (2 * fetch_kb + write_kb) * 1024
+    out = {"kernel": "k_env_step", "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section)",
+           "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_env_step": round(hbm / E, 1), "envs_per_launch": E}
+    json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
+    print("== HBM traffic per k_env_step launch:", json.dumps(out))
+sq = {}
+for r in rows("sq"):
+    if "k_env_step" in r["Kernel_Name"]:
+        sq.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+if sq:
+    w = sum(sq["SQ_WAVES"]) / len(sq["SQ_WAVES"])
+    print("== SQ counters per wave (k_env_step):",
+          {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(sq.items()) if k != "SQ_WAVES"})
