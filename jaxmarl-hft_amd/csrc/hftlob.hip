@@ -1471,6 +1471,72 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     R.agentQuant = aq; R.qp_agent = qp;
 }
 
+// ------------------------------------------------------- step PRNG (VALU)
+// Every key of one step, derived lane-parallel: lanes compute different
+// threefry blocks at once, in VALU (the scalar unit is the shared resource of
+// a CU; one threefry2x32-20 is ~100 instructions).  Derivation, as the
+// scalar form in hftlob_sample_actions / k_env_step used it:
+//   key        = keys[e], or split(master, n_env + 1)[e + 1] (rollout mode)
+//   k1, key_reset = split(key)                           (marl_env.py:787)
+//   sub        = split(split(k1)[1])[1]; bits[l] = random_bits(sub, A)[l]
+//                (jax.random.permutation of the action rows, marl_env.py:293-295)
+//   actions    = randint(split(split(key, n_types)[t], n_agents_t)[i], 0, n_actions_t)
+//                (Speed_test.py:166-177), agent ag's in lane 32 + ag
+struct StepKeys {
+    Key key_reset;
+    u32 shuffle_bits;  // lane l < A: random word of action row l
+    i32 acts;          // lane 32 + ag: sampled action (rollout mode)
+};
+// agent lane 32 + ag -> (type, index within type)
+DEV void agent_of_lane(const hftlob_env_cfg& c, int ag, int& t, int& i) {
+    t = 0;
+    i = ag;
+#pragma unroll
+    for (int k = 0; k < HFTLOB_MAX_TYPES - 1; ++k)
+        if (k < c.n_types - 1 && i >= c.types[t].n_agents) { i -= c.types[t].n_agents; ++t; }
+}
+DEV Key lane_key(Key v) { return Key{(u32)rdl((i32)v.a, 0), (u32)rdl((i32)v.b, 0)}; }
+DEV Key from_lane(Key v, int src) {  // per-lane gather v[src]
+    return Key{(u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.a), (u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.b)};
+}
+DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* keys, const u32* master, u32* master_out) {
+    const bool part = c.prng_partitionable;
+    const int l = lane_id(), nTy = c.n_types, A = c.n_action_msgs;
+    Key key;
+    if (master) {  // lane 0: this env's key; lane 1: the carried master key
+        const Key mk{master[0], master[1]};
+        const Key v = split_key(mk, n_env + 1, l == 0 ? e + 1 : 0, part);
+        key = lane_key(v);
+        if ((e == 0) & (l == 1)) { master_out[0] = v.a; master_out[1] = v.b; }
+    } else {
+        key = Key{keys[2 * e], keys[2 * e + 1]};
+    }
+    const int ag = l - 32;
+    int t = 0, i = 0;
+    agent_of_lane(c, ag < 0 ? 0 : ag, t, i);
+    const bool agent_lane = (ag >= 0) & (ag < c.n_agents);
+    // L1: lane 0 k1, lane 1 key_reset, lane 2+t split(key, n_types)[t]
+    const Key L1 = split_key(key, l < 2 ? 2 : nTy, l < 2 ? l : l - 2, part);
+    StepKeys o;
+    o.key_reset = Key{(u32)rdl((i32)L1.a, 1), (u32)rdl((i32)L1.b, 1)};
+    // L2: lane 0 sk = split(k1)[1]; agent lanes: split(sub_t, n_agents_t)[i]
+    const Key P2 = from_lane(L1, agent_lane ? 2 + t : 0);
+    const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
+    // L3: lane 0 sub = split(sk)[1]; agent lanes: randint's two keys
+    const Key L3a = split_key(L2, 2, l == 0 ? 1 : 0, part);
+    const Key L3b = split_key(L2, 2, 1, part);
+    // L4: lanes < A: random_bits(sub, A)[l]; agent lanes: the two randint words
+    const Key sub = from_lane(L3a, 0);
+    o.shuffle_bits = random_bits(sub, A > 0 ? A : 1, l < A ? l : 0, part);
+    const u32 hb = random_bits(L3a, 1, 0, part), lb = random_bits(L3b, 1, 0, part);
+    const i32 na = agent_lane ? c.types[t].n_actions : 1;
+    const u32 span = na <= 0 ? 1u : (u32)na;  // randint(key, 0, n_actions)
+    u32 mult = 65536u % span;
+    mult = (mult * mult) % span;
+    o.acts = (i32)(((hb % span) * mult + (lb % span)) % span);
+    return o;
+}
+
 // ====================================================== K2: fused env step
 // MARLEnv.step — marl_env.py:775-804 (step_env :211-709, auto-reset select)
 #define MAX_AGENT_ROWS 128
@@ -1493,7 +1559,6 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     if (e >= n_env) return;
     STAMP(t_start);
     const int l = lane_id();
-    const bool part = c.prng_partitionable;
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
     i32* rec = state + (size_t)e * c.rec_words;
     // LDS: [agent rows (C+A)*8][action extras n_agents*6, 16B-padded][book]
@@ -1504,19 +1569,8 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     if (NFIX > 0) { B.c.nO = NFIX; B.c.nT = NFIX; }
     const int R = B.c.nO;
     book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
-    Key key;
-    if (master) {
-        const Key mk{master[0], master[1]};
-        key = split_key(mk, n_env + 1, e + 1, part);
-        if ((e == 0) & (l == 0)) {
-            const Key k0 = split_key(mk, n_env + 1, 0, part);
-            master_out[0] = k0.a;
-            master_out[1] = k0.b;
-        }
-    } else {
-        key = Key{keys[2 * e], keys[2 * e + 1]};
-    }
-    const Key k1 = split_key(key, 2, 0, part), key_reset = split_key(key, 2, 1, part);
+    const StepKeys SK = step_keys(c, n_env, e, keys, master, master_out);
+    const Key key_reset = SK.key_reset;
     // loaded / world scalars (wave-uniform)
     const i32* Lr = rec + c.off_loaded;
     const i32* Wr = rec + c.off_world;
@@ -1548,9 +1602,8 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             for (int i = 0; i < tc.n_agents; ++i, ++ag) {
                 const i32 tid = wsub(tc.trader_id0, i);
                 i32 act;
-                if (master) {  // Speed_test.py:166-177 (as k_sample_actions)
-                    const Key sub = split_key(key, c.n_types, t, part);
-                    act = randint(split_key(sub, tc.n_agents, i, part), 0, tc.n_actions, part);
+                if (master) {  // Speed_test.py:166-177, sampled by step_keys
+                    act = rdl(SK.acts, 32 + ag);
                     if (actions_io && l == 0) actions_io[(size_t)e * c.n_agents + ag] = act;
                 } else {
                     act = actions_io[(size_t)e * c.n_agents + ag];
@@ -1598,9 +1651,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         }
         int dest = l;
         if (c.shuffle_action_messages && A >= 2) {
-            const Key sk = split_key(k1, 2, 1, part);
-            const Key sub = split_key(sk, 2, 1, part);
-            const u32 bits = random_bits(sub, A, l, part);
+            const u32 bits = SK.shuffle_bits;
             int rank = 0;
             for (int j = 0; j < A; ++j) {
                 const u32 bj = (u32)rdl((i32)bits, j);

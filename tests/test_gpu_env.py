@@ -68,10 +68,10 @@ def _day(w, mid, seed=11):
     return _DAYS[key]
 
 
-def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11):
+def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True):
     w = cfg.world_config
     day = _day(w, mid, seed)
-    env = MARLEnv(None, cfg, data=day)
+    env = MARLEnv(None, cfg, data=day, prng_partitionable=partitionable)
     params = env.default_params
     init = O.init_states(env.cfg_c.lob, env.windows, day.msgs, w, env.layout.init_rec_words)
     assert (init == env._init_states.cpu().numpy()).all()
@@ -84,7 +84,7 @@ def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11):
                            [env.layout.obs_dims[t] for t in env.layout.agent_types])], 1), rtol=RTOL, atol=1e-6)
     rng = keys
     for k in range(K):
-        nk = split_keys(rng, 2)
+        nk = split_keys(rng, 2, partitionable)
         rng, sk = nk[:, 0].contiguous(), nk[:, 1].contiguous()
         acts = env.sample_actions(sk)
         o_acts = O.sample_actions(env.cfg_c, sk.cpu().numpy().view(np.uint32))
@@ -115,6 +115,12 @@ def test_env_rollout_parity(name, mid):
     rollout_parity(builtin_config(name), mid)
 
 
+@pytest.mark.parametrize("name", ["2_player_fq_fqc", "3_player_fq_fqc_dir"])
+def test_env_rollout_parity_legacy_prng(name):
+    """jax_threefry_partitionable=False (the pre-0.5 JAX default) split / random_bits."""
+    rollout_parity(builtin_config(name), E=32, K=66, partitionable=False)
+
+
 MM_VARIANTS = [
     dict(reward_function=r) for r in ("portfolio_value", "buy_sell_pnl", "complex", "zero_inv", "spooner",
                                       "spooner_damped", "spooner_asym_damped", "spooner_scaled",
@@ -143,11 +149,13 @@ def test_exe_option_parity(changes):
     rollout_parity(variant(builtin_config("2_player_fq_fqc"), "Execution", **changes), E=32, K=66)
 
 
-def test_step_sampled_equals_split_sample_step():
+@pytest.mark.parametrize("name,part", [("2_player_fq_fqc", True), ("3_player_fq_fqc_dir", True),
+                                       ("2_player_fq_fqc", False)])
+def test_step_sampled_equals_split_sample_step(name, part):
     """hftlob_env_step_sampled (one launch) == split_keys + sample_actions + env_step."""
-    cfg = builtin_config("2_player_fq_fqc")
+    cfg = builtin_config(name)
     w = cfg.world_config
-    env = MARLEnv(None, cfg, data=_day(w, 2_000_000))
+    env = MARLEnv(None, cfg, data=_day(w, 2_000_000), prng_partitionable=part)
     params = env.default_params
     E = 48
     keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
@@ -161,7 +169,7 @@ def test_step_sampled_equals_split_sample_step():
         o1 = [x.clone() for x in o1]
         r1 = [x.clone() for x in r1]
         da1 = d1["__all__"].clone()
-        ks = split_keys(rng, E + 1)[0]
+        ks = split_keys(rng, E + 1, part)[0]
         rng, sk = ks[0:1].contiguous(), ks[1:].contiguous()
         acts = env.sample_actions(sk)
         o2, s2, r2, d2, _ = env.step(sk, s2, acts, params)
