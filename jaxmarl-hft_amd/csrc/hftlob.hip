@@ -269,11 +269,10 @@ template <int S> DEV int first_true(const bool (&pr)[S], int fallback) {
 }
 // value of (uniform) slot e from a column held lane-strided in registers
 template <int S> DEV i32 sget(const i32 (&a)[S], int e) {
-    const int l = e & 63;
-    i32 v = rdl(a[0], l);
+    i32 v = a[0];  // pick the register set (v_cndmask on a uniform condition), then one v_readlane
 #pragma unroll
-    for (int k = 1; k < S; ++k) v = (e >> 6) == k ? rdl(a[k], l) : v;
-    return v;
+    for (int k = 1; k < S; ++k) v = (e >> 6) == k ? a[k] : v;
+    return rdl(v, e & 63);
 }
 
 template <int S>
@@ -521,10 +520,18 @@ template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq
 template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i32 dq) {
     constexpr u32 OK = SideBits<ASKS>::OK;
     if (!(fl & OK)) return;
-    if (op == -1 || s.best_p == -1) { fl &= ~OK; return; }
-    if (op != s.best_p) return;
-    s.best_q = wsub(s.best_q, dq);
-    if (s.best_q <= 0) fl &= ~OK;  // level exhausted (or odd data): rescan
+    if (op == s.best_p) {
+        if (op == -1) {
+            fl &= ~OK;
+        } else {
+            s.best_q = wsub(s.best_q, dq);
+            if (s.best_q <= 0) fl &= ~OK;  // level exhausted (or odd data): rescan
+        }
+    } else if (op == -1) {
+        fl &= ~OK;
+    } else if (s.best_p == -1) {
+        fl &= ~OK;
+    }
 }
 
 // match_order — JaxOrderBookArrays.py:172-220
@@ -1571,6 +1578,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
     const StepKeys SK = step_keys(c, n_env, e, keys, master, master_out);
     const Key key_reset = SK.key_reset;
+    STAMP(t_keys);
     // loaded / world scalars (wave-uniform)
     const i32* Lr = rec + c.off_loaded;
     const i32* Wr = rec + c.off_world;
@@ -1592,6 +1600,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     }
     B.fl = load_side<true>(B.a, rec + c.off_asks, R, B.vs) | load_side<false>(B.b, rec + c.off_bids, R, B.vs);
     B.fl |= fast_bit(B.fl);
+    STAMP(t_load);
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
     {
@@ -1640,6 +1649,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         }
     }
     __syncthreads();
+    STAMP(t_rows);
     // order ids (counter - j) and the action-row permutation (lane j = action row j)
     {
         i32 f[8];
@@ -1834,6 +1844,8 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
         info[0] = (i32)(t_agents - t_start); info[1] = (i32)(t_book - t_agents);
         info[2] = (i32)(t_rewards - t_book); info[3] = (i32)(t_end - t_rewards); info[4] = (i32)all;
+        info[5] = (i32)(t_keys - t_start); info[6] = (i32)(t_load - t_keys); info[7] = (i32)(t_rows - t_load);
+        info[8] = (i32)(t_agents - t_rows);
     }
 #endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs

@@ -29,17 +29,18 @@ params = env.default_params
 E = 4096
 keys = split_keys(torch.tensor([[0, 0]], dtype=torch.int32, device="cuda"), E + 1)[0][1:].contiguous()
 _, state = env.reset(keys, params)
-rng = torch.tensor([[0, 1]], dtype=torch.int32, device="cuda")
+kbuf = [torch.tensor([0, 1], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
 rows = []
 for k in range(80):
-    ks = split_keys(rng, E + 1)[0]
-    rng, sk = ks[0:1].contiguous(), ks[1:].contiguous()
-    env.step(sk, state, env.sample_actions(sk), params)
+    env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)   # the bench's path
     if k >= 8:
-        rows.append(env._out["info"][:, :5].cpu().numpy().copy())
+        rows.append(env._out["info"][:, :9].cpu().numpy().copy())
 r = np.concatenate(rows).astype(np.int64)
 names = ["setup+agent msgs+shuffle", "112-msg book loop", "rewards+state+obs", "store+info"]
 tot = r[:, :4].sum(1)
 print(f"env-steps sampled: {len(r)}; median total cycles/env-step: {np.median(tot):.0f}")
 for i, n in enumerate(names):
     print(f"  {n:28s} median {np.median(r[:, i]):9.0f}  mean {r[:, i].mean():9.0f}  share {r[:, i].sum() / tot.sum():.3f}")
+for i, n in zip(range(5, 9), ["  setup: step keys (PRNG)", "  setup: load book sides", "  setup: agent rows",
+                             "  setup: ids + shuffle"]):
+    print(f"  {n:28s} median {np.median(r[:, i]):9.0f}  mean {r[:, i].mean():9.0f}")
