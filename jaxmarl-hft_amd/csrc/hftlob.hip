@@ -300,28 +300,50 @@ DEV u32 fast_bit(u32 fl) {
     return (fl & (F_CLEAN_A | F_CLEAN_B | F_NEG1_A | F_NEG1_B)) == (F_CLEAN_A | F_CLEAN_B) ? F_FAST : 0u;
 }
 
-// global [R][6] rows -> LDS side table; returns the side's CLEAN / NEG1 bits
-template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
+// A side's rows in registers between the global load and the LDS commit, so
+// the HBM latency of the load can overlap other work.
+template <int S>
+struct SideRows {
+    int2 x0[S], x1[S], x2[S];  // (p, q), (oid, tid), (ts, tns) of slot r*64+lane
+};
+template <int S> DEV void fetch_side(SideRows<S>& f, const i32* g, const Valid<S>& V) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        f.x0[r] = f.x1[r] = f.x2[r] = make_int2(-1, -1);
+        if (V.v[r]) {
+            const int2* row = reinterpret_cast<const int2*>(g + (r * 64 + l) * 6);
+            f.x0[r] = row[0]; f.x1[r] = row[1]; f.x2[r] = row[2];
+        }
+    }
+}
+// fetched rows -> LDS side table; returns the side's CLEAN / NEG1 bits.  The
+// per-row "any field == -1" / "all fields == -1" tests run as unsigned min /
+// max of the complemented fields (VALU), not as chains of lane-mask logic.
+template <bool ASKS, int S> DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) {
     const int l = lane_id();
     lmask bad = 0, n1 = 0;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         const int sl = r * 64 + l;
-        i32 p = -1, q = -1, oid = -1, tid = -1, ts = -1, tns = -1;
+        const i32 p = f.x0[r].x, q = f.x0[r].y, oid = f.x1[r].x, tid = f.x1[r].y, ts = f.x2[r].x, tns = f.x2[r].y;
         if (V.v[r]) {
-            const int2* row = reinterpret_cast<const int2*>(g + sl * 6);
-            int2 x0 = row[0], x1 = row[1], x2 = row[2];
-            p = x0.x; q = x0.y; oid = x1.x; tid = x1.y; ts = x2.x; tns = x2.y;
             i32* t = s.t + sl;
             t[FP * R] = p; t[FQ * R] = q; t[FOID * R] = oid; t[FTID * R] = tid; t[FTS * R] = ts; t[FTNS * R] = tns;
         }
-        const lmask any = bal(p == -1) | bal(q == -1) | bal(oid == -1) | bal(tid == -1) | bal(ts == -1) | bal(tns == -1);
-        const lmask all = bal(p == -1) & bal(q == -1) & bal(oid == -1) & bal(tid == -1) & bal(ts == -1) & bal(tns == -1);
-        bad |= V.m[r] & bal(q <= 0) & ~all;
-        n1 |= V.m[r] & ~bal(p == -1) & any;
+        const u32 np = ~(u32)p, nq = ~(u32)q, no = ~(u32)oid, nt = ~(u32)tid, ns = ~(u32)ts, nn = ~(u32)tns;
+        const u32 any0 = min(min(min(np, nq), min(no, nt)), min(ns, nn));  // 0 <=> some field == -1
+        const u32 all0 = max(max(max(np, nq), max(no, nt)), max(ns, nn));  // 0 <=> every field == -1
+        bad |= V.m[r] & bal((q <= 0) & (all0 != 0u));
+        n1 |= V.m[r] & bal((p != -1) & (any0 == 0u));
     }
     lds_order();
     return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u);
+}
+template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
+    SideRows<S> f;
+    fetch_side(f, g, V);
+    return commit_side<ASKS>(s, f, R, V);
 }
 template <int S> DEV void store_side(const Side<S>& s, i32* g, int R, const Valid<S>& V) {
     const int l = lane_id();
@@ -1031,16 +1053,18 @@ template <int S>
 DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int size, i32 side, i32 t, i32 tns,
                      i32* lds_rows, int row0) {
     int n = 0;
-    i32 tid[S];
+    i32 tid[S], q[S], p[S], o[S];  // one LDS round trip; hit rows are read from registers
     ldcol(s.t, R, FTID, tid);
+    ldcol(s.t, R, FQ, q);
+    ldcol(s.t, R, FP, p);
+    ldcol(s.t, R, FOID, o);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         lmask bm = V.m[r] & bal(tid[r] == agent);
         while (bm && n < size) {
-            const int e = r * 64 + (int)__builtin_ctzll(bm);
+            const int ln = (int)__builtin_ctzll(bm);
             bm &= bm - 1;
-            put_row(lds_rows, row0 + n, 2, side, ldu(s.t, R, FQ, e), ldu(s.t, R, FP, e), ldu(s.t, R, FOID, e),
-                    agent, t, tns);
+            put_row(lds_rows, row0 + n, 2, side, rdl(q[r], ln), rdl(p[r], ln), rdl(o[r], ln), agent, t, tns);
             ++n;
         }
     }
@@ -1576,6 +1600,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     if (NFIX > 0) { B.c.nO = NFIX; B.c.nT = NFIX; }
     const int R = B.c.nO;
     book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
+    SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
+    fetch_side(fa, rec + c.off_asks, B.vs);
+    fetch_side(fb, rec + c.off_bids, B.vs);
     const StepKeys SK = step_keys(c, n_env, e, keys, master, master_out);
     const Key key_reset = SK.key_reset;
     STAMP(t_keys);
@@ -1598,7 +1625,17 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             excl_any = ballot(any) != 0ull;
         }
     }
-    B.fl = load_side<true>(B.a, rec + c.off_asks, R, B.vs) | load_side<false>(B.b, rec + c.off_bids, R, B.vs);
+    // the data window (BaseLOBEnv.get_data_messages, base_env.py:339-369); its
+    // first chunk is fetched now, ahead of the agent phase
+    i32 dstart = wadd(start_index, wmul(D, step));
+    dstart = imax_(0, imin_(dstart, c.n_data_rows - D));  // dynamic_slice clamping
+    int4 px = make_int4(0, 0, 0, 0), py = px;
+    if ((l >= C + A) & (l < M)) {
+        const i32* g = msg_data + (size_t)(dstart + l - (C + A)) * 8;
+        px = reinterpret_cast<const int4*>(g)[0];
+        py = reinterpret_cast<const int4*>(g)[1];
+    }
+    B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs);
     B.fl |= fast_bit(B.fl);
     STAMP(t_load);
 
@@ -1680,8 +1717,6 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     STAMP(t_agents);
     // ---- (B)+(D) stream the combined messages through the book, 64 per chunk
     trades_fill(B.tr, B.vt, -1);
-    i32 dstart = wadd(start_index, wmul(D, step));
-    dstart = imax_(0, imin_(dstart, c.n_data_rows - D));  // dynamic_slice clamping
     const int AR = C + A;
     bool abort_any = false;
     i32 prev_a = -1, prev_b = -1;
@@ -1693,6 +1728,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         if (row < AR) {
             x = reinterpret_cast<const int4*>(rows + row * 8)[0];
             y = reinterpret_cast<const int4*>(rows + row * 8)[1];
+        } else if (base == 0) {
+            x = px;
+            y = py;
         } else if (row < M) {
             const i32* g = msg_data + (size_t)(dstart + row - AR) * 8;
             x = reinterpret_cast<const int4*>(g)[0];
