@@ -105,8 +105,10 @@ DEV unsigned long long ballot(bool p) { return __ballot(p); }
 // k_env_step, written to the info buffer in place of the info fields.
 #ifdef HFTLOB_STAMPS
 #define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define STAMP_ACC(acc, since) acc += __builtin_amdgcn_s_memtime() - since
 #else
 #define STAMP(var)
+#define STAMP_ACC(acc, since)
 #endif
 
 // ------------------------------------------------------------------ PRNG
@@ -1046,7 +1048,6 @@ DEV void put_row(i32* lds_rows, int row, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4,
     v = l == 4 ? f4 : v; v = l == 5 ? f5 : v; v = l == 6 ? f6 : v; v = l == 7 ? f7 : v;
     if (l < 8) lds_rows[row * 8 + l] = v;
 }
-DEV i32 get_field(const i32* lds_rows, int row, int f) { return uni(lds_rows[row * 8 + f]); }
 
 // getCancelMsgs — JaxOrderBookArrays.py:827-853
 template <int S>
@@ -1071,52 +1072,46 @@ DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int 
     for (; n < size; ++n) put_row(lds_rows, row0 + n, 2, side, 0, 0, 0, 0, t, tns);
 }
 
-// _filter_messages — mm_env.py:520-582 == exec_env.py:413-475 (N rows, scalar)
+// _filter_messages — mm_env.py:520-582 == exec_env.py:413-475, lane-parallel:
+// lane i < n holds action row arow + i, lane 8 + j cancel row crow + j.
+// Action i and cancel j match when their prices agree and the price is not 0;
+// the k-th matched action pairs with the k-th matched cancel (in row order),
+// rel[k] = (cv[k] >= av[k]) ? av[k] : 0 over the zero-padded k-th matched
+// quantities, and every row subtracts rel[its rank] (unmatched rows rank after
+// the matched ones).  Action rows left with quantity 0 become all-zero rows.
+// `scratch`: 16 words of LDS.
 template <int n>
-DEV void filter_rows(i32* lds_rows, int arow, int crow) {
+DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
     __syncthreads();
-    i32 ap[n], aqv[n], cp[n], cq[n];
-    for (int i = 0; i < n; ++i) {
-        ap[i] = get_field(lds_rows, arow + i, 3); aqv[i] = get_field(lds_rows, arow + i, 2);
-        cp[i] = get_field(lds_rows, crow + i, 3); cq[i] = get_field(lds_rows, crow + i, 2);
-    }
-    bool am[n], cm[n];
-    for (int i = 0; i < n; ++i) { am[i] = false; cm[i] = false; }
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j)
-            if (cp[j] == ap[i] && ap[i] != 0) { am[i] = true; cm[j] = true; }
-    // k-th matched quantity (zero-padded), without runtime array indexing
-    i32 av[n], cv[n], rel[n];
+    const int l = lane_id();
+    const bool is_a = l < n, is_c = (l >= 8) & (l < 8 + n);
+    const int row = is_a ? arow + l : (is_c ? crow + l - 8 : arow);
+    const i32 p = lds_rows[row * 8 + 3], q = lds_rows[row * 8 + 2];
+    lmask ma = 0, mc = 0;
 #pragma unroll
     for (int k = 0; k < n; ++k) {
-        i32 va = 0, vc = 0;
-        int ka = 0, kc = 0;
-#pragma unroll
-        for (int i = 0; i < n; ++i) {
-            if (am[i]) { if (ka == k) va = aqv[i]; ++ka; }
-            if (cm[i]) { if (kc == k) vc = cq[i]; ++kc; }
-        }
-        av[k] = va;
-        cv[k] = vc;
+        const i32 cpk = rdl(p, 8 + k), apk = rdl(p, k);
+        ma |= bal(is_a & (p != 0) & (p == cpk));
+        mc |= bal(is_c & (apk != 0) & (p == apk));
     }
-    for (int i = 0; i < n; ++i) rel[i] = (cv[i] >= av[i]) ? av[i] : 0;
-    int na = 0, nc = 0;
-    for (int i = 0; i < n; ++i) { na += am[i]; nc += cm[i]; }
-    int ta = 0, fa = 0, tcn = 0, fc = 0;
-    const int l = lane_id();
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-        const int ra = am[i] ? ta++ : na + fa++;
-        i32 rra = 0, rrc = 0;
-#pragma unroll
-        for (int k = 0; k < n; ++k) if (k == ra) rra = rel[k];
-        const i32 nq = wsub(aqv[i], rra);
-        if (nq == 0) { if (l < 8) lds_rows[(arow + i) * 8 + l] = 0; }
-        else if (l == 0) lds_rows[(arow + i) * 8 + 2] = nq;
-        const int rc = cm[i] ? tcn++ : nc + fc++;
-#pragma unroll
-        for (int k = 0; k < n; ++k) if (k == rc) rrc = rel[k];
-        if (l == 0) lds_rows[(crow + i) * 8 + 2] = wsub(cq[i], rrc);
+    constexpr lmask amask = (1ull << n) - 1, cmask = amask << 8;
+    const int na = __builtin_popcountll(ma), nc = __builtin_popcountll(mc);
+    const lmask mine = is_a ? ma : mc, all = is_a ? amask : cmask;
+    const bool matched = (mine >> l) & 1ull;
+    const lmask below = matched ? mine : (~mine & all);
+    const int cnt = (int)__builtin_amdgcn_mbcnt_hi((u32)(below >> 32), __builtin_amdgcn_mbcnt_lo((u32)below, 0u));
+    const int rank = matched ? cnt : (is_a ? na : nc) + cnt;
+    if (l < 16) scratch[l] = 0;  // av[k] = scratch[k], cv[k] = scratch[8 + k]
+    lds_order();
+    if ((is_a | is_c) & matched) scratch[(is_c ? 8 : 0) + rank] = q;
+    lds_order();
+    const i32 av = scratch[rank & 7], cv = scratch[8 + (rank & 7)];
+    const i32 nq = wsub(q, cv >= av ? av : 0);
+    if (is_a & (nq == 0)) {
+        reinterpret_cast<int4*>(lds_rows + row * 8)[0] = make_int4(0, 0, 0, 0);
+        reinterpret_cast<int4*>(lds_rows + row * 8)[1] = make_int4(0, 0, 0, 0);
+    } else if (is_a | is_c) {
+        lds_rows[row * 8 + 2] = nq;
     }
     __syncthreads();
 }
@@ -1640,6 +1635,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     STAMP(t_load);
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
+#ifdef HFTLOB_STAMPS
+    unsigned long long acc_act = 0, acc_cnl = 0, acc_flt = 0;
+#endif
     {
         int ag = 0, arow = C, crow = 0;
         const i32* st = rec + c.off_agents;
@@ -1656,20 +1654,28 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                 }
                 i32 s4[4] = {st[0], st[1], st[2], st[3]};
                 ActX x{0, 0, 0, 0, 0, 0};
+                STAMP(ta0);
                 if (tc.kind == HFTLOB_AGENT_MM) {
                     if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
                         mm_directional(c, tc, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
                     else
                         mm_fixed_quant(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
+                    STAMP_ACC(acc_act, ta0);
+                    STAMP(ta1);
                     const int sz = tc.n_msgs / 4;
                     cancel_rows(B.b, R, B.vs, tid, sz, 1, wt0, wt1, rows, crow);
                     cancel_rows(B.a, R, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
+                    STAMP_ACC(acc_cnl, ta1);
                 } else {
                     exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow);
+                    STAMP_ACC(acc_act, ta0);
+                    STAMP(ta1);
                     const i32 sell = s4[3];
                     cancel_rows(sell ? B.a : B.b, R, B.vs, tid, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
                                 crow);
+                    STAMP_ACC(acc_cnl, ta1);
                 }
+                STAMP(ta2);
                 {
                     const i32 xv[6] = {x.bid_price, x.ask_price, x.bid_dist, x.ask_dist, x.bid_quant, x.ask_quant};
                     i32 v = 0;
@@ -1677,8 +1683,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                     for (int k = 0; k < 6; ++k) if (l == k) v = xv[k];
                     if (l < 6) axs[ag * 6 + l] = v;
                 }
-                if (tc.kind == HFTLOB_AGENT_MM) filter_rows<2>(rows, arow, crow);
-                else filter_rows<4>(rows, arow, crow);
+                if (tc.kind == HFTLOB_AGENT_MM) filter_rows<2>(rows, arow, crow, B.a.scr);
+                else filter_rows<4>(rows, arow, crow, B.a.scr);
+                STAMP_ACC(acc_flt, ta2);
                 arow += tc.n_action_msgs;
                 crow += tc.n_msgs - tc.n_action_msgs;
                 st += agent_words(tc);
@@ -1884,6 +1891,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         info[2] = (i32)(t_rewards - t_book); info[3] = (i32)(t_end - t_rewards); info[4] = (i32)all;
         info[5] = (i32)(t_keys - t_start); info[6] = (i32)(t_load - t_keys); info[7] = (i32)(t_rows - t_load);
         info[8] = (i32)(t_agents - t_rows);
+        info[9] = (i32)acc_act; info[10] = (i32)acc_cnl; info[11] = (i32)acc_flt;
     }
 #endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
