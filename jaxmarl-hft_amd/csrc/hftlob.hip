@@ -1,16 +1,18 @@
 // hftlob.hip — MI355X (gfx950 / CDNA4) limit-order-book engine and fused
 // multi-agent env step, behind the C ABI of include/hftlob.h.
 //
-// Execution model: ONE 64-lane wavefront per environment.  An order-book side
-// of nO slots lives in VGPRs lane-strided (slot s -> lane s&63, register set
-// s>>6, S = ceil(nO/64) sets), the trade log likewise, and the message stream
-// is held 64 rows at a time (row m -> lane m&63).  Each message is decoded into
-// SGPRs with v_readlane, so the per-message type dispatch is a wave-uniform
-// scalar branch (only the taken handler runs — the XLA reference evaluates all
-// five lax.switch branches under vmap).  Price-time priority, first-free-slot,
-// best-quote and volume queries are DPP wave reductions and ballots.  Single
-// slots are updated with v_writelane.  No LDS for book state; a 4 KB LDS
-// staging area holds the agents' message rows of the fused step.
+// Execution model: ONE 64-lane wavefront per environment.  The book lives in
+// LDS as structure-of-arrays tables (per side [6 fields][nO slots], trade log
+// [8][nT]); slot s maps to lane s&63, register set s>>6 when a column is
+// loaded.  The message stream is taken 64 rows at a time (row m -> lane m&63),
+// decoded for the whole chunk in VALU, and each message is read into SGPRs
+// with v_readlane, so the per-message dispatch is a wave-uniform scalar branch
+// (only the taken handler runs — the XLA reference evaluates all five
+// lax.switch branches under vmap).  Price-time priority, first-free-slot,
+// best-quote and volume queries are DPP wave reductions and ballots.
+// The CU's single scalar ALU, shared by its 16 resident waves, is the scarce
+// resource: the code keeps per-lane work in VALU and uniform state in one
+// flag word.
 //
 // Semantics follow the reference line by line (cited per function), including
 // its quirks.  Integer state is bit-exact with the
