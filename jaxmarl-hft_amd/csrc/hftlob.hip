@@ -17,7 +17,7 @@
 // Semantics follow the reference line by line (cited per function), including
 // its quirks.  Integer state is bit-exact with the
 // oracle; float32 arithmetic follows the jnp expression order, and float sums
-// use the canonical wave order (fold lane l+64k, then xor butterfly 32..1).
+// use the canonical wave order (fold lane l+64k, then xor butterfly 1..32).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -95,11 +95,20 @@ DEV i32 wave_sum(i32 v) {
     v = wadd(v, DPPX(0, v, 0x143, 0xC));
     return rdl(v, 63);
 }
-// canonical float sum (order fixed; the C oracle emulates it bit for bit)
+// canonical float sum: xor-butterfly order 1, 2, 4, 8, 16, 32 (the C oracle
+// emulates it bit for bit).  Done with DPP: quad_perm xor1 / xor2, then
+// row_half_mirror and row_mirror (equal to xor4 / xor8 once each quad / half
+// row holds one value; float + commutes exactly), then row_bcast15 / 31 into
+// lane 63.  No LDS round trip.
+#define FDPP(v, ctrl, rmask) __int_as_float(DPPX(0, __float_as_int(v), ctrl, rmask))
 DEV float wave_fsum(float v) {
-#pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) v = v + __shfl_xor(v, k, 64);
-    return unif(v);
+    v = v + FDPP(v, 0xB1, 0xF);
+    v = v + FDPP(v, 0x4E, 0xF);
+    v = v + FDPP(v, 0x141, 0xF);
+    v = v + FDPP(v, 0x140, 0xF);
+    v = v + FDPP(v, 0x142, 0xA);
+    v = v + FDPP(v, 0x143, 0xC);
+    return __int_as_float(rdl(__float_as_int(v), 63));
 }
 DEV unsigned long long ballot(bool p) { return __ballot(p); }
 
@@ -530,16 +539,19 @@ struct Msg {
 template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq, i32 maxint) {
     // an all -1 row now holds (np, nq > 0)
     constexpr u32 OK = SideBits<!BID>::OK;
-    if (!(fl & OK)) return;
-    if (BID) {
-        if (s.best_p == -1) {
-            if (np > -1) { s.best_p = np; s.best_q = nq; } else fl &= ~OK;
-        } else if (np > s.best_p) { s.best_p = np; s.best_q = nq; }
-        else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
-    } else {
-        if (np == -1 || np == maxint) { if (s.best_p == -1) fl &= ~OK; return; }
-        if (s.best_p == -1 || np < s.best_p) { s.best_p = np; s.best_q = nq; }
-        else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
+    if (fl & OK) {
+        if (BID) {
+            if (s.best_p == -1) {
+                if (np > -1) { s.best_p = np; s.best_q = nq; } else fl &= ~OK;
+            } else if (np > s.best_p) { s.best_p = np; s.best_q = nq; }
+            else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
+        } else if ((np == -1) | (np == maxint)) {
+            if (s.best_p == -1) fl &= ~OK;
+        } else if ((s.best_p == -1) | (np < s.best_p)) {
+            s.best_p = np; s.best_q = nq;
+        } else if (np == s.best_p) {
+            s.best_q = wadd(s.best_q, nq);
+        }
     }
 }
 // a row at price op lost dq of its quantity (possibly all of it)
@@ -608,16 +620,17 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
 }
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
-// p, q: the side's price and quantity columns (loaded by the caller)
+// p, q: the side's price and quantity columns, free: its p == -1 slots (from the caller)
 template <bool BID, bool G, int S>
-DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)[S], const i32 (&q)[S]) {
+DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)[S], const i32 (&q)[S],
+                   const lmask (&free)[S]) {
     const int R = B.c.nO;
     lmask fm[S];
     constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK;
     const bool fast = !G || ((B.fl & (CLEAN | NEG1)) == CLEAN);  // then "any -1" <=> p == -1
     if (fast) {
 #pragma unroll
-        for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == -1);
+        for (int r = 0; r < S; ++r) fm[r] = free[r];
     } else {
         i32 o[S], t[S], ts[S], tn[S];
         ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
@@ -649,12 +662,9 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)
 
 // check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max);
 // p is the side's price column, reloaded here if rows were cleared
-template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&p)[S], i32 (&q)[S]) {
+template <bool BID, int S>
+DEV void evict_worst(Book<S>& B, Side<S>& s, i32 (&p)[S], i32 (&q)[S], lmask (&free)[S]) {
     const int R = B.c.nO;
-    lmask neg = 0;
-#pragma unroll
-    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(p[r] < 0);
-    if (neg != 0ull) return;
     i32 w = BID ? INT_MAX : INT_MIN;
 #pragma unroll
     for (int r = 0; r < S; ++r)
@@ -667,27 +677,50 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&
     B.fl &= ~SideBits<!BID>::OK;
     ldcol(s.t, R, FP, p);
     ldcol(s.t, R, FQ, q);
+#pragma unroll
+    for (int r = 0; r < S; ++r) free[r] = B.vs.m[r] & bal(p[r] == -1);
 }
 
+// (called when no slot holds p == -1; `free` is then recomputed after a clear)
+template <bool BID, int S>
+DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&p)[S], i32 (&q)[S], lmask (&free)[S]) {
+    lmask neg = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(p[r] < 0);
+    if (neg == 0ull) evict_worst<BID>(B, s, p, q, free);
+}
+// the side's price / quantity columns and its p == -1 slots
+template <int S> DEV void load_pq_free(const Book<S>& B, const Side<S>& s, i32 (&p)[S], i32 (&q)[S], lmask (&free)[S]) {
+    ldcol(s.t, B.c.nO, FP, p);
+    ldcol(s.t, B.c.nO, FQ, q);
+#pragma unroll
+    for (int r = 0; r < S; ++r) free[r] = B.vs.m[r] & bal(p[r] == -1);
+}
+template <int S> DEV bool no_slot(const lmask (&m)[S]) {
+    lmask a = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) a |= m[r];
+    return a == 0ull;
+}
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
     i32 p[S], q[S];
-    ldcol(B.b.t, B.c.nO, FP, p);
-    ldcol(B.b.t, B.c.nO, FQ, q);
-    if (B.c.check_fill) evict_if_full<true>(B, B.b, p, q);
-    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, p, q);
+    lmask free[S];
+    load_pq_free(B, B.b, p, q, free);
+    if (B.c.check_fill && no_slot(free)) evict_if_full<true>(B, B.b, p, q, free);
+    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, p, q, free);
 }
 // ask_lim — :446-508
 template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (B.c.t4 == 2) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
     i32 p[S], q[S];
-    ldcol(B.a.t, B.c.nO, FP, p);
-    ldcol(B.a.t, B.c.nO, FQ, q);
-    if (B.c.check_fill) evict_if_full<false>(B, B.a, p, q);
-    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p, q);
+    lmask free[S];
+    load_pq_free(B, B.a, p, q, free);
+    if (B.c.check_fill && no_slot(free)) evict_if_full<false>(B, B.a, p, q, free);
+    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p, q, free);
 }
 // cancel_order + get_init_id_match — :93-139
 template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {

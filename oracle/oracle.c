@@ -67,7 +67,8 @@ static inline float bitf(i32 w) { float f; memcpy(&f, &w, 4); return f; }
 static inline i32 fbit(float f) { i32 w; memcpy(&w, &f, 4); return w; }
 
 /* canonical wave-order float sum: lane l folds x[l], x[l+64], x[l+128], ...
- * in that order, then an xor-butterfly over the 64 lanes (k = 32 .. 1) */
+ * in that order, then an xor-butterfly over the 64 lanes (k = 1, 2, .. 32;
+ * the HIP kernel's DPP reduction gives exactly this tree at lane 63) */
 static float wsum(const float* x, int n) {
     float v[64];
     for (int l = 0; l < 64; ++l) {
@@ -75,12 +76,12 @@ static float wsum(const float* x, int n) {
         for (int j = l + 64; j < n; j += 64) a = a + x[j];
         v[l] = a;
     }
-    for (int k = 32; k >= 1; k >>= 1) {
+    for (int k = 1; k <= 32; k <<= 1) {  /* xor butterfly 1, 2, 4, 8, 16, 32 */
         float t[64];
         for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ k];
         memcpy(v, t, sizeof v);
     }
-    return v[0];
+    return v[63];
 }
 
 /* ================================================================= PRNG */
