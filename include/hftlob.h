@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HFTLOB_ABI_VERSION 2
+#define HFTLOB_ABI_VERSION 3
 
 #define HFTLOB_OK            0
 #define HFTLOB_EINVAL      (-1)   /* bad config value / unsupported option */
@@ -54,11 +54,13 @@ typedef struct hftlob_lob_cfg {
     int32_t maxint;                /* 2147483647 */
     int32_t init_id;               /* -2 */
     int32_t book_depth;            /* 10 */
-    int32_t cancel_mode;           /* 0 STRICT_BY_ID, 1 INCLUDE_INITS (2/3 unsupported) */
+    int32_t cancel_mode;           /* 0 STRICT_BY_ID, 1 INCLUDE_INITS, 2 RANDOM, 3 RANDOM_LARGE */
     int32_t type_4_interpretation; /* 0 IOC, 1 LIM, 2 MKT */
     int32_t check_book_fill;       /* bool */
     int32_t n_orders;              /* slots per book side (nOrders) */
     int32_t n_trades;              /* trade-log rows (nTrades) */
+    int32_t prng_partitionable;    /* cancel_mode 2/3 draws: jax_threefry_partitionable (env cfg: equal to
+                                      hftlob_env_cfg.prng_partitionable) */
 } hftlob_lob_cfg;
 
 /* ---- agent kinds and the option enums (jaxen/mm_env.py, jaxen/exec_env.py) */
@@ -175,7 +177,7 @@ typedef struct hftlob_env_cfg {
     int32_t off_asks, off_bids, off_trades, off_loaded;
     int32_t off_best_bids, off_best_asks, off_world, off_agents;
     int32_t info_words;            /* words per env in the optional info buffer */
-    int32_t _pad[3];
+    int32_t _pad[2];
     hftlob_agent_type_cfg types[HFTLOB_MAX_TYPES];
 } hftlob_env_cfg;
 
@@ -207,8 +209,11 @@ const char* hftlob_last_error(void);
  * asks,bids [n_env][n_orders][6]   in/out
  * trades    [n_env][n_trades][8]   in/out (caller initialises, e.g. all -1)
  * best_asks,best_bids [n_env][n_msg][2] out: (price, qty) after every message,
- *           NULL for both = scan_through_entire_array (no per-message output). */
-int hftlob_book_process(const hftlob_lob_cfg* cfg /*[host]*/, int n_env, int n_msg,
+ *           NULL for both = scan_through_entire_array (no per-message output).
+ * keys      uint32 [n_env][2]: the scan's `key` argument; message k draws from
+ *           split(key, n_msg)[k] (get_random_id_match, :141-164).  Only read
+ *           for cancel_mode 2/3; may be NULL otherwise. */
+int hftlob_book_process(const hftlob_lob_cfg* cfg /*[host]*/, int n_env, int n_msg, const uint32_t* keys,
                         const int32_t* msgs, int32_t* asks, int32_t* bids, int32_t* trades,
                         int32_t* best_asks, int32_t* best_bids, void* stream);
 

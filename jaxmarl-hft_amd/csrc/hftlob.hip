@@ -525,6 +525,11 @@ struct Book {
     Valid<S> vs, vt;
     LobCfg c;
     u32 fl;  // F_* bits
+    // cancel_mode 2/3 only (RC instantiations): the scan's key and the index
+    // of the message being processed (keys = split(ek, nmsg); key i is message i's)
+    Key ek;
+    i32 mi, nmsg;
+    bool part;
 };
 
 // message handler codes (the reference's dispatch index) and flags, see decode_msgs
@@ -722,8 +727,47 @@ template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (B.c.check_fill && no_slot(free)) evict_if_full<false>(B, B.a, p, q, free);
     if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p, q, free);
 }
-// cancel_order + get_init_id_match — :93-139
-template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+// get_random_id_match / get_random_large_id_match — :141-164 (cancel_mode 2/3).
+// key = split(key)[0]; chosen = jax.random.choice(key, ids, p=|sign(ids)|),
+// ids = the row's order id where `pm` holds, else 0.  choice with p (JAX):
+// r = cumsum(p)[-1] * (1 - uniform_f32(key)), ind = searchsorted(cumsum(p), r)
+// (side='left').  The weights are 0/1, so the float cumsum is exact and ind is
+// the K-th weighted row, K = ceil(r) (ind = 0, chosen = 0, when no row weighs).
+// idx = first row whose id == chosen (any row, as jnp.where(ids == chosen)).
+template <int S>
+DEV int random_id_match(const Book<S>& B, Key& k, const i32 (&o)[S], const lmask (&pm)[S]) {
+    k = split_key(k, 2, 0, B.part);
+    lmask w[S];
+    int tot = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        w[r] = pm[r] & bal(o[r] != 0);
+        tot += __builtin_popcountll(w[r]);
+    }
+    const u32 bits = random_bits(k, 1, 0, B.part);
+    const float u = __uint_as_float((bits >> 9) | 0x3f800000u) - 1.0f;
+    const float rr = (float)tot * (1.0f - u);
+    i32 chosen = 0;
+    if (tot > 0) {
+        int K = (int)ceilf(rr);
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const int c = __builtin_popcountll(w[r]);
+            if (K > 0 && K <= c) {
+                const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(w[r] >> 32), __builtin_amdgcn_mbcnt_lo((u32)w[r], 0u));
+                const lmask hit = w[r] & bal(below == (u32)(K - 1));
+                chosen = rdl(o[r], (int)ff1(hit));
+            }
+            K -= c;
+        }
+    }
+    lmask f[S];
+#pragma unroll
+    for (int r = 0; r < S; ++r) f[r] = B.vs.m[r] & bal(o[r] == chosen);
+    return first_slot(f, -1);
+}
+// cancel_order + get_init_id_match — :93-139 (+ :141-164 when RC)
+template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     const int R = B.c.nO;
     i32 o[S], p[S], q[S];
     ldcol(s.t, R, FOID, o);
@@ -739,7 +783,23 @@ template <bool G, bool ASKS, int S> DEV void cancel(Book<S>& B, Side<S>& s, cons
         for (int r = 0; r < S; ++r)
             fm[r] = B.vs.m[r] & bal(p[r] == m.price) & bal(o[r] <= B.c.init_id) & bal(o[r] >= lo) &
                     bal(q[r] >= m.qty);
-        idx = first_slot(fm, R - 1);  // -1 wraps to the last slot
+        if (!RC) {
+            idx = first_slot(fm, R - 1);  // -1 wraps to the last slot
+        } else {
+            idx = first_slot(fm, -1);
+            if (idx < 0 && B.c.cancel_mode >= 2) {
+                Key k = split_key(B.ek, B.nmsg, B.mi, B.part);
+#pragma unroll
+                for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == m.price) & bal(q[r] >= m.qty);
+                idx = random_id_match(B, k, o, fm);
+                if (idx < 0 && B.c.cancel_mode == 3) {
+#pragma unroll
+                    for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == m.price);
+                    idx = random_id_match(B, k, o, fm);
+                }
+            }
+            if (idx < 0) idx = R - 1;
+        }
     }
     const i32 op = sget(p, idx), oq = sget(q, idx);
     const i32 nq = wsub(oq, m.qty);
@@ -776,19 +836,20 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     x.x = h;
     x.y = sd;
 }
-template <bool G, int S>
+template <bool G, bool RC, int S>
 DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
     m.h = h; m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
     const i32 kind = h & H_KIND;
-    if (kind == H_CNL_ASK) cancel<G, true>(B, B.a, m);
-    else if (kind == H_CNL_BID) cancel<G, false>(B, B.b, m);
+    if (kind == H_CNL_ASK) cancel<G, true, RC>(B, B.a, m);
+    else if (kind == H_CNL_BID) cancel<G, false, RC>(B, B.b, m);
     else if (kind == H_BID) bid_lim<G>(B, m);
     else if (kind == H_ASK) ask_lim<G>(B, m);
 }
-template <int S> DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
-    if (B.fl & F_FAST) process_msg_<false>(B, h, d1, d2, d3, d4, d5, d6, d7);
-    else process_msg_<true>(B, h, d1, d2, d3, d4, d5, d6, d7);
+template <bool RC, int S>
+DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+    if (B.fl & F_FAST) process_msg_<false, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
+    else process_msg_<true, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
 }
 // forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
 DEV i32 ffill(i32 v, i32 carry) {
@@ -820,8 +881,10 @@ template <int S> DEV void book_bind(Book<S>& B, i32* lds) {
 
 // ================================================= K1: book_process kernel
 // scan_through_entire_array[_save_bidask] — JaxOrderBookArrays.py:736-823
-template <int S>
-__global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const i32* __restrict__ msgs,
+// RC: cancel_mode 2/3 (keys[e] is the scan's key; message k uses split(key, n_msg)[k])
+template <int S, bool RC>
+__global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_env, int n_msg, const u32* __restrict__ keys,
+                                                     const i32* __restrict__ msgs,
                                                      i32* __restrict__ asks, i32* __restrict__ bids,
                                                      i32* __restrict__ trades, i32* __restrict__ best_asks,
                                                      i32* __restrict__ best_bids) {
@@ -839,6 +902,11 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs);
     B.fl |= fast_bit(B.fl);
     load_trades(B.tr, gt, B.vt);
+    if (RC) {
+        B.ek = Key{keys[2 * e], keys[2 * e + 1]};
+        B.nmsg = n_msg;
+        B.part = cfg.prng_partitionable;
+    }
     const i32* gm = msgs + (size_t)e * n_msg * 8;
     for (int base = 0; base < n_msg; base += 64) {
         const int row = base + l;
@@ -851,8 +919,9 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
         i32 ap = 0, aq = 0, bp = 0, bq = 0;
         const int cnt = imin_(64, n_msg - base);
         for (int k = 0; k < cnt; ++k) {
-            process_msg(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
-                        rdl(y.z, k), rdl(y.w, k));
+            if (RC) B.mi = base + k;
+            process_msg<RC>(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
+                            rdl(y.z, k), rdl(y.w, k));
             if (best_asks) {
                 refresh_best(B);
                 ap = wlane(ap, B.a.best_p, k); aq = wlane(aq, B.a.best_q, k);
@@ -1544,7 +1613,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 //   actions    = randint(split(split(key, n_types)[t], n_agents_t)[i], 0, n_actions_t)
 //                (Speed_test.py:166-177), agent ag's in lane 32 + ag
 struct StepKeys {
-    Key key_reset;
+    Key k1, key_reset;
     u32 shuffle_bits;  // lane l < A: random word of action row l
     i32 acts;          // lane 32 + ag: sampled action (rollout mode)
 };
@@ -1579,6 +1648,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     // L1: lane 0 k1, lane 1 key_reset, lane 2+t split(key, n_types)[t]
     const Key L1 = split_key(key, l < 2 ? 2 : nTy, l < 2 ? l : l - 2, part);
     StepKeys o;
+    o.k1 = Key{(u32)rdl((i32)L1.a, 0), (u32)rdl((i32)L1.b, 0)};
     o.key_reset = Key{(u32)rdl((i32)L1.a, 1), (u32)rdl((i32)L1.b, 1)};
     // L2: lane 0 sk = split(k1)[1]; agent lanes: split(sub_t, n_agents_t)[i]
     const Key P2 = from_lane(L1, agent_lane ? 2 + t : 0);
@@ -1603,7 +1673,8 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
 #define MAX_AGENT_ROWS 128
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
-template <int S, int NFIX>
+template <int S, int NFIX, bool RC>
+// RC: cancel_mode 2/3 (the random cancel fallback of the engine).
 // master != NULL: Speed_test rollout mode — the env's step key is
 // split(master, n_env + 1)[e + 1], actions are sampled here (hftlob_sample_actions)
 // and written to actions_io if it is not NULL; env 0 writes split(master)[0]
@@ -1635,6 +1706,11 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     fetch_side(fb, rec + c.off_bids, B.vs);
     const StepKeys SK = step_keys(c, n_env, e, keys, master, master_out);
     const Key key_reset = SK.key_reset;
+    if (RC) {  // the scan's key: k1, or split(k1)[0] after the shuffle split (marl_env.py:293-294,349-351)
+        B.ek = c.shuffle_action_messages ? split_key(SK.k1, 2, 0, c.prng_partitionable) : SK.k1;
+        B.nmsg = M;
+        B.part = c.prng_partitionable;
+    }
     STAMP(t_keys);
     // loaded / world scalars (wave-uniform)
     const i32* Lr = rec + c.off_loaded;
@@ -1782,8 +1858,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
         const int cnt = imin_(64, M - base);
         for (int k = 0; k < cnt; ++k) {
-            process_msg(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k), rdl(y.z, k),
-                        rdl(y.w, k));
+            if (RC) B.mi = base + k;
+            process_msg<RC>(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
+                            rdl(y.z, k), rdl(y.w, k));
             refresh_best(B);
             rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
             rpb = wlane(rpb, B.b.best_p, k); rqb = wlane(rqb, B.b.best_q, k);
@@ -1978,7 +2055,7 @@ const char* hftlob_last_error(void) { return g_err; }
 
 static int check_lob(const hftlob_lob_cfg* c) {
     if (!c) return fail(HFTLOB_ENULL, "null cfg");
-    if (c->cancel_mode < 0 || c->cancel_mode > 1) return fail(HFTLOB_EINVAL, "cancel_mode 2/3 (random cancel) unsupported");
+    if (c->cancel_mode < 0 || c->cancel_mode > 3) return fail(HFTLOB_EINVAL, "bad cancel_mode");
     if (c->type_4_interpretation < 0 || c->type_4_interpretation > 2) return fail(HFTLOB_EINVAL, "bad type_4_interpretation");
     if (c->n_orders < 1 || c->n_orders > HFTLOB_MAX_SLOTS || c->n_trades < 1 || c->n_trades > HFTLOB_MAX_SLOTS)
         return fail(HFTLOB_ESHAPE, "n_orders / n_trades out of range");
@@ -1990,21 +2067,33 @@ static int launch_status() {
     return HFTLOB_OK;
 }
 
-int hftlob_book_process(const hftlob_lob_cfg* cfg, int n_env, int n_msg, const int32_t* msgs, int32_t* asks,
-                        int32_t* bids, int32_t* trades, int32_t* best_asks, int32_t* best_bids, void* stream) {
+int hftlob_book_process(const hftlob_lob_cfg* cfg, int n_env, int n_msg, const uint32_t* keys, const int32_t* msgs,
+                        int32_t* asks, int32_t* bids, int32_t* trades, int32_t* best_asks, int32_t* best_bids,
+                        void* stream) {
     int rc = check_lob(cfg);
     if (rc) return rc;
     if (n_env < 0 || n_msg < 0) return fail(HFTLOB_ESHAPE, "negative size");
     if (n_env == 0) return HFTLOB_OK;
     if (!asks || !bids || !trades || (n_msg > 0 && !msgs)) return fail(HFTLOB_ENULL, "null array");
     if ((best_asks == nullptr) != (best_bids == nullptr)) return fail(HFTLOB_ENULL, "best_asks/best_bids: both or none");
+    const bool rc_ = cfg->cancel_mode >= 2;
+    if (rc_ && !keys) return fail(HFTLOB_ENULL, "keys required for cancel_mode 2/3");
     const int S = slot_sets(cfg->n_orders > cfg->n_trades ? cfg->n_orders : cfg->n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
     const size_t shm = 4 * ((size_t)12 * cfg->n_orders + 8 * cfg->n_trades + 64 * 4);
-    if (S == 1) hipLaunchKernelGGL(k_book_process<1>, g, b, shm, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
-    else if (S == 2) hipLaunchKernelGGL(k_book_process<2>, g, b, shm, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
-    else hipLaunchKernelGGL(k_book_process<4>, g, b, shm, st, *cfg, n_env, n_msg, msgs, asks, bids, trades, best_asks, best_bids);
+#define LAUNCH_BOOK(SS, RC) hipLaunchKernelGGL((k_book_process<SS, RC>), g, b, shm, st, *cfg, n_env, n_msg, keys, msgs, \
+                                               asks, bids, trades, best_asks, best_bids)
+    if (rc_) {
+        if (S == 1) LAUNCH_BOOK(1, true);
+        else if (S == 2) LAUNCH_BOOK(2, true);
+        else LAUNCH_BOOK(4, true);
+    } else {
+        if (S == 1) LAUNCH_BOOK(1, false);
+        else if (S == 2) LAUNCH_BOOK(2, false);
+        else LAUNCH_BOOK(4, false);
+    }
+#undef LAUNCH_BOOK
     return launch_status();
 }
 
@@ -2013,6 +2102,7 @@ static int check_env(const hftlob_env_cfg* c) {
     int rc = check_lob(&c->lob);
     if (rc) return rc;
     if (c->ep_type != 0) return fail(HFTLOB_EINVAL, "only ep_type fixed_steps is supported");
+    if (c->lob.prng_partitionable != c->prng_partitionable) return fail(HFTLOB_EINVAL, "lob.prng_partitionable differs");
     if (c->n_types < 1 || c->n_types > HFTLOB_MAX_TYPES || c->n_agents < 1 || c->n_agents > HFTLOB_MAX_AGENTS)
         return fail(HFTLOB_ESHAPE, "agent counts out of range");
     if (c->n_msgs < 1 || c->n_msgs > HFTLOB_MAX_MSGS || c->n_action_msgs > 64 ||
@@ -2063,13 +2153,17 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, const uint32_t*
     dim3 g(n_env), b(64);
     const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
                             12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
-#define LAUNCH_STEP(SS, NF) hipLaunchKernelGGL((k_env_step<SS, NF>), g, b, shm, st, *cfg, n_env, keys, key_in, key_out, \
+#define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, *cfg, n_env, keys, key_in, key_out, \
                                                actions, msg_data, init_states, state, out->obs, out->rewards, \
                                                out->done_all, out->dones, out->info)
-    if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100);
-    else if (S == 1) LAUNCH_STEP(1, 0);
-    else if (S == 2) LAUNCH_STEP(2, 0);
-    else LAUNCH_STEP(4, 0);
+    if (cfg->lob.cancel_mode >= 2) {  // random cancel fallback: general sizes only
+        if (S == 1) LAUNCH_STEP(1, 0, true);
+        else if (S == 2) LAUNCH_STEP(2, 0, true);
+        else LAUNCH_STEP(4, 0, true);
+    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100, false);
+    else if (S == 1) LAUNCH_STEP(1, 0, false);
+    else if (S == 2) LAUNCH_STEP(2, 0, false);
+    else LAUNCH_STEP(4, 0, false);
 #undef LAUNCH_STEP
     return launch_status();
 }

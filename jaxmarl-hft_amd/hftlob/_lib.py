@@ -12,7 +12,7 @@ import os
 from .layout import EnvCfg, LobCfg, StepOut
 
 LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
            "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_sample_actions", "hftlob_split_keys")
 
@@ -35,7 +35,7 @@ def lib() -> C.CDLL:
     vp, i32 = C.c_void_p, C.c_int
     L.hftlob_version.restype = i32
     L.hftlob_last_error.restype = C.c_char_p
-    L.hftlob_book_process.argtypes = [C.POINTER(LobCfg), i32, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.hftlob_book_process.argtypes = [C.POINTER(LobCfg), i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     L.hftlob_book_process.restype = i32
     L.hftlob_env_reset.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp, vp, C.POINTER(StepOut), vp]
     L.hftlob_env_reset.restype = i32

@@ -157,6 +157,7 @@ class MARLEnv:
         self.data = data
         self.windows: Windows = make_windows(data, w)
         self.n_windows = len(self.windows.starts)
+        self.prng_partitionable = prng_partitionable
         self.cfg_c, self.layout = pack_env_cfg(cfg, self.n_windows, data.msgs.shape[0], prng_partitionable)
         L = self.layout
         self.num_msgs_per_step = L.n_msgs
@@ -179,7 +180,9 @@ class MARLEnv:
         asks = torch.full((W, w.nOrders, 6), -1, dtype=torch.int32, device=dev)
         bids = torch.full_like(asks, -1)
         trades = torch.full((W, w.nTrades, 8), -1, dtype=torch.int32, device=dev)
-        book_process_(w, im.contiguous(), asks, bids, trades)
+        # the init orders are limit adds only, so the scan key (cancel_mode 2/3) is never drawn from
+        keys = torch.zeros((W, 2), dtype=torch.int32, device=dev)
+        book_process_(w, im.contiguous(), asks, bids, trades, keys=keys, prng_partitionable=self.prng_partitionable)
         rows = loaded_rows(asks.cpu().numpy(), bids.cpu().numpy(), trades.cpu().numpy(), first_times,
                            self.windows, w.n_data_msg_per_step, L.init_rec_words)
         return torch.from_numpy(rows).to(dev)

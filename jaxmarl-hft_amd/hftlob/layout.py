@@ -30,7 +30,8 @@ AGENT_MM, AGENT_EXE = 0, 1
 class LobCfg(C.Structure):
     _fields_ = [("maxint", C.c_int32), ("init_id", C.c_int32), ("book_depth", C.c_int32),
                 ("cancel_mode", C.c_int32), ("type_4_interpretation", C.c_int32),
-                ("check_book_fill", C.c_int32), ("n_orders", C.c_int32), ("n_trades", C.c_int32)]
+                ("check_book_fill", C.c_int32), ("n_orders", C.c_int32), ("n_trades", C.c_int32),
+                ("prng_partitionable", C.c_int32)]
 
 
 class AgentTypeCfg(C.Structure):
@@ -57,7 +58,7 @@ class EnvCfg(C.Structure):
         "shuffle_action_messages", "prng_partitionable", "n_types", "n_agents", "obs_stride",
         "rec_words", "init_rec_words", "off_asks", "off_bids", "off_trades", "off_loaded",
         "off_best_bids", "off_best_asks", "off_world", "off_agents", "info_words")] + [
-        ("_pad", C.c_int32 * 3), ("types", AgentTypeCfg * MAX_TYPES)]
+        ("_pad", C.c_int32 * 2), ("types", AgentTypeCfg * MAX_TYPES)]
 
 
 class StepOut(C.Structure):
@@ -237,15 +238,16 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
     return a
 
 
-def pack_lob_cfg(w) -> LobCfg:
+def pack_lob_cfg(w, prng_partitionable: bool = True) -> LobCfg:
     if w.simulator_mode != 0:
         raise NotImplementedError("simulator_mode LOBSTER_INTERPRETER is not implemented (reference: NotImplementedError)")
-    if w.cancel_mode not in (0, 1):
-        raise NotImplementedError("cancel_mode 2/3 (random cancel matching) not implemented")
+    if w.cancel_mode not in (0, 1, 2, 3):
+        raise ValueError(f"cancel_mode {w.cancel_mode} (jaxob_constants.CancelMode has 0..3)")
     c = LobCfg()
     c.maxint, c.init_id, c.book_depth = w.maxint, w.init_id, w.book_depth
     c.cancel_mode, c.type_4_interpretation = w.cancel_mode, w.type_4_interpretation
     c.check_book_fill, c.n_orders, c.n_trades = int(w.check_book_fill), w.nOrders, w.nTrades
+    c.prng_partitionable = int(prng_partitionable)
     return c
 
 
@@ -256,7 +258,7 @@ def pack_env_cfg(cfg: MultiAgentConfig, n_windows: int, n_data_rows: int,
     if len(cfg.dict_of_agents_configs) > MAX_TYPES or len(L.agent_kinds) > MAX_AGENTS:
         raise ValueError("too many agent types / agents")
     c = EnvCfg()
-    c.lob = pack_lob_cfg(w)
+    c.lob = pack_lob_cfg(w, prng_partitionable)
     c.n_data_msg, c.n_msgs, c.n_action_msgs, c.n_cancel_msgs = L.n_data_msg, L.n_msgs, L.n_action_msgs, L.n_cancel_msgs
     c.tick_size, c.ep_type, c.episode_time = w.tick_size, 0, w.episode_time
     c.window_selector, c.n_windows, c.n_data_rows = w.window_selector, n_windows, n_data_rows

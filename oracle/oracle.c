@@ -24,7 +24,7 @@
  * Float arithmetic is float32, op for op as XLA would evaluate the jnp
  * expressions (int32 operands promoted to f32, weak-typed Python constants
  * staying f32).  Float sums use the canonical "wave order" (fold element
- * l+64 into l, then xor-butterfly 32..1) so this checker matches the HIP path
+ * l+64 into l, then xor-butterfly 1, 2, .., 32) so this checker matches the HIP path
  * bit for bit; the reference's own XLA order is unknowable, hence
  * the 1e-5 tolerance in the tests against the reference-order numpy oracle.
  * Build: cc -O2 -fopenmp -ffp-contract=off (see oracle/Makefile).
@@ -200,8 +200,47 @@ static void add_order(i32* s, int nO, const Msg* m) {
     remove_zero_neg(s, nO);
 }
 
-/* cancel_order + get_init_id_match — :93-139 (cancel_mode 0/1) */
-static void cancel_order(const hftlob_lob_cfg* c, i32* s, const Msg* m) {
+/* get_random_id_match (large = 0) / get_random_large_id_match (large = 1) —
+ * :141-164.  key <- split(key, 2)[0]; order_ids = where(price match [& qty >=
+ * msg qty], oid, 0); chosen = jax.random.choice(key, order_ids,
+ * p=|sign(order_ids)|), which for p given and shape () is
+ *   p_cuml = cumsum(p) (float32); r = p_cuml[-1] * (1 - uniform(key));
+ *   ind = searchsorted(p_cuml, r, side='left'); chosen = order_ids[ind]
+ * (jax/_src/random.py choice; uniform = bits >> 9 | 1.0f, minus 1).  Then idx =
+ * first row with oid == chosen, or -1. */
+static int random_id_match(const hftlob_lob_cfg* c, u32* key, const i32* s, const Msg* m, int large) {
+    int nO = c->n_orders, part = c->prng_partitionable;
+    u32 k[2];
+    oracle_split(key, 2, 0, part, k);
+    key[0] = k[0];
+    key[1] = k[1];
+    i32 ids[HFTLOB_MAX_SLOTS];
+    float cum[HFTLOB_MAX_SLOTS], acc = 0.0f;
+    for (int i = 0; i < nO; ++i) {
+        const i32* r = s + i * 6;
+        int pm = r[0] == m->price && (large || r[1] >= m->qty);
+        ids[i] = pm ? r[2] : 0;
+        acc += (float)iabs(isign(ids[i]));
+        cum[i] = acc;
+    }
+    u32 bits = random_bits_i(key, 1, 0, part), fb = (bits >> 9) | 0x3f800000u;
+    float u;
+    memcpy(&u, &fb, 4);
+    u -= 1.0f;
+    float r = cum[nO - 1] * (1.0f - u);
+    int ind = 0;
+    while (ind < nO && cum[ind] < r) ++ind;  /* searchsorted, side='left' */
+    if (ind >= nO) ind = nO - 1;             /* unreachable: r <= cum[-1] */
+    i32 chosen = ids[ind];
+    for (int i = 0; i < nO; ++i)
+        if (s[i * 6 + 2] == chosen) return i;
+    return -1;
+}
+
+/* cancel_order + get_init_id_match — :93-139; cancel_mode 2/3 fall back to
+ * the random matches (:130-136,149-154) drawing from `key` (the scan key of
+ * this message, split(key, M)[k], :753,784,816) */
+static void cancel_order(const hftlob_lob_cfg* c, i32* s, const Msg* m, const u32* msg_key) {
     int nO = c->n_orders, idx = -1;
     for (int i = 0; i < nO; ++i)
         if (s[i * 6 + 2] == m->oid) { idx = i; break; }
@@ -210,6 +249,11 @@ static void cancel_order(const hftlob_lob_cfg* c, i32* s, const Msg* m) {
         for (int i = 0; i < nO; ++i) {
             const i32* r = s + i * 6;
             if (r[0] == m->price && r[2] <= c->init_id && r[2] >= lo && r[1] >= m->qty) { idx = i; break; }
+        }
+        if (idx == -1 && c->cancel_mode >= 2) {
+            u32 k[2] = {msg_key[0], msg_key[1]};
+            idx = random_id_match(c, k, s, m, 0);
+            if (idx == -1 && c->cancel_mode == 3) idx = random_id_match(c, k, s, m, 1);
         }
     }
     if (idx == -1) idx = nO - 1; /* negative index wraps to the last slot */
@@ -335,7 +379,12 @@ static void best_quotes(const hftlob_lob_cfg* c, const i32* asks, const i32* bid
 }
 
 /* cond_type_side_save_bidask — :687-732 (GENERAL_EXCHANGE mode) */
-static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* bids, i32* trades) {
+/* scan_key / n_msg / k: the scan's key and this message's position (the key
+ * is split(scan_key, n_msg)[k]; only drawn from under cancel_mode 2/3) */
+static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* bids, i32* trades,
+                        const u32* scan_key, int n_msg, int k) {
+    u32 mk[2] = {0u, 0u};
+    if (c->cancel_mode >= 2) oracle_split(scan_key, n_msg, k, c->prng_partitionable, mk);
     Msg m;
     m.type = d[0];
     m.side = d[0] == 4 ? wsub(0, d[1]) : d[1];
@@ -346,28 +395,29 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
     switch (index) {
         case 0: ask_lim(c, m, asks, bids, trades); break;
         case 1: bid_lim(c, m, asks, bids, trades); break;
-        case 2: cancel_order(c, asks, &m); break;
-        case 3: cancel_order(c, bids, &m); break;
+        case 2: cancel_order(c, asks, &m, mk); break;
+        case 3: cancel_order(c, bids, &m, mk); break;
         default: break; /* doNothing */
     }
 }
 
 static int lob_cfg_ok(const hftlob_lob_cfg* c) {
-    return c->cancel_mode >= 0 && c->cancel_mode <= 1 && c->type_4_interpretation >= 0 &&
+    return c->cancel_mode >= 0 && c->cancel_mode <= 3 && c->type_4_interpretation >= 0 &&
            c->type_4_interpretation <= 2 && c->n_orders > 0 && c->n_orders <= HFTLOB_MAX_SLOTS &&
            c->n_trades > 0 && c->n_trades <= HFTLOB_MAX_SLOTS;
 }
 
 /* scan_through_entire_array[_save_bidask] — :736-823, batched over envs (host memory) */
-int oracle_book_process(const hftlob_lob_cfg* c, int n_env, int n_msg, const i32* msgs, i32* asks,
+int oracle_book_process(const hftlob_lob_cfg* c, int n_env, int n_msg, const u32* keys, const i32* msgs, i32* asks,
                         i32* bids, i32* trades, i32* best_asks, i32* best_bids) {
     if (!lob_cfg_ok(c)) return HFTLOB_EINVAL;
+    if (c->cancel_mode >= 2 && !keys) return HFTLOB_ENULL;
     int nO = c->n_orders, nT = c->n_trades;
 #pragma omp parallel for schedule(dynamic, 16)
     for (int e = 0; e < n_env; ++e) {
         i32 *a = asks + (size_t)e * nO * 6, *b = bids + (size_t)e * nO * 6, *tr = trades + (size_t)e * nT * 8;
         for (int k = 0; k < n_msg; ++k) {
-            process_msg(c, msgs + ((size_t)e * n_msg + k) * 8, a, b, tr);
+            process_msg(c, msgs + ((size_t)e * n_msg + k) * 8, a, b, tr, keys ? keys + 2 * e : NULL, n_msg, k);
             if (best_asks)
                 best_quotes(c, a, b, best_asks + ((size_t)e * n_msg + k) * 2, best_bids + ((size_t)e * n_msg + k) * 2);
         }
@@ -1039,10 +1089,12 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     i32 new_ctr = wsub(ctr, A);
     int perm[HFTLOB_MAX_MSGS];
     for (int j = 0; j < A; ++j) perm[j] = j;
+    const u32* scan_key = k1; /* marl_env.py:293-294: key, shuffle_key = split(key); scan(key) :349-351 */
     if (c->shuffle_action_messages) {
         oracle_split(k1, 2, 0, part, k2);
         oracle_split(k1, 2, 1, part, shuffle_key);
         oracle_permutation(shuffle_key, A, part, perm);
+        scan_key = k2;
     }
     memcpy(comb, cnlm, (size_t)C * 8 * sizeof(i32));
     for (int j = 0; j < A; ++j) memcpy(comb + (size_t)(C + j) * 8, actm + (size_t)perm[j] * 8, 8 * sizeof(i32));
@@ -1053,7 +1105,7 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     for (int i = 0; i < nT * 8; ++i) trades[i] = -1;
     i32 bba[HFTLOB_MAX_MSGS * 2], bbb[HFTLOB_MAX_MSGS * 2];
     for (int m = 0; m < M; ++m) {
-        process_msg(&c->lob, comb + m * 8, asks, bids, trades);
+        process_msg(&c->lob, comb + m * 8, asks, bids, trades, scan_key, M, m);
         best_quotes(&c->lob, asks, bids, bba + m * 2, bbb + m * 2);
     }
     int abort_ep = 0;

@@ -29,7 +29,7 @@ def lib():
             build()
         L = C.CDLL(LIB)
         vp = C.c_void_p
-        L.oracle_book_process.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
+        L.oracle_book_process.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
         L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
@@ -79,14 +79,17 @@ def split_keys(keys, n, partitionable=True):
     return out
 
 
-def book_process(lob_cfg, msgs, asks, bids, trades, save_best=True):
-    """scan_through_entire_array[_save_bidask] over a batch; returns new arrays."""
+def book_process(lob_cfg, msgs, asks, bids, trades, save_best=True, keys=None):
+    """scan_through_entire_array[_save_bidask] over a batch; returns new arrays.
+    keys: uint32 [E, 2] scan keys (cancel_mode 2/3); None = all-zero keys."""
     msgs = np.ascontiguousarray(msgs, dtype=np.int32)
+    keys = (np.zeros((msgs.shape[0], 2), np.uint32) if keys is None
+            else np.ascontiguousarray(keys, dtype=np.uint32).reshape(msgs.shape[0], 2))
     asks, bids, trades = (np.array(x, dtype=np.int32, copy=True, order="C") for x in (asks, bids, trades))
     E, M = msgs.shape[0], msgs.shape[1]
     ba = np.zeros((E, M, 2), dtype=np.int32) if save_best else None
     bb = np.zeros((E, M, 2), dtype=np.int32) if save_best else None
-    _chk(lib().oracle_book_process(C.byref(lob_cfg), E, M, _p(msgs), _p(asks), _p(bids), _p(trades), _p(ba), _p(bb)))
+    _chk(lib().oracle_book_process(C.byref(lob_cfg), E, M, _p(keys), _p(msgs), _p(asks), _p(bids), _p(trades), _p(ba), _p(bb)))
     return asks, bids, trades, ba, bb
 
 

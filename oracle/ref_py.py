@@ -38,10 +38,41 @@ def get_init_id_match(cfg, side, msg):          # :120-139
     return _first(m)
 
 
-def cancel_order(cfg, side, msg):               # :93-117
+def _uniform_f32(key, partitionable):
+    """jax.random.uniform(key, (), float32): (bits >> 9 | 1.0f) - 1."""
+    y0, y1 = threefry2x32(key[0], key[1], 0, 0)
+    bits = (y0 ^ y1) if partitionable else y0
+    return np.array([(bits >> 9) | 0x3F800000], np.uint32).view(np.float32)[0] - np.float32(1.0)
+
+
+def _choice_p(key, a, p, partitionable):
+    """jax.random.choice(key, a, p=p) for shape=(), replace=True (jax/_src/random.py)."""
+    p_cuml = np.cumsum(np.asarray(p, np.float32), dtype=np.float32)
+    r = np.float32(p_cuml[-1] * (np.float32(1.0) - _uniform_f32(key, partitionable)))
+    ind = int(np.searchsorted(p_cuml, r, side="left"))
+    return a[ind]
+
+
+def get_random_id_match(cfg, key, side, msg, large=False):   # :141-164
+    part = cfg.get("partitionable", True)
+    key = split(key, 2, part)[0]
+    pm = side[:, 0] == msg["price"]
+    if not large:
+        pm = pm & (side[:, 1] >= msg["quantity"])
+    ids = np.where(pm, side[:, 2], 0).astype(I32)
+    chosen = _choice_p(key, ids, np.abs(np.sign(ids)), part)
+    idx = _first(side[:, 2] == chosen)
+    if idx == -1 and not large and cfg["cancel_mode"] == 3:
+        idx = get_random_id_match(cfg, key, side, msg, large=True)
+    return idx
+
+
+def cancel_order(cfg, side, msg, key=None):     # :93-117
     idx = _first(side[:, 2] == msg["orderid"])
     if idx == -1:
         idx = get_init_id_match(cfg, side, msg)
+        if idx == -1 and cfg["cancel_mode"] in (2, 3):
+            idx = get_random_id_match(cfg, key, side, msg)
     side = side.copy()
     side[idx, 1] = np.int32(side[idx, 1] - msg["quantity"])
     return remove_zero_neg(side)
@@ -100,7 +131,7 @@ def _lim(cfg, msg, own, opp, trades, own_is_bid):
     return added, opp, trades
 
 
-def process_msg(cfg, book, data):               # cond_type_side_save_bidask :687-732
+def process_msg(cfg, book, data, key=None):     # cond_type_side_save_bidask :687-732
     asks, bids, trades = book
     msg = {"side": -int(data[1]) if data[0] == 4 else int(data[1]), "type": int(data[0]), "price": int(data[3]),
            "quantity": int(data[2]), "orderid": int(data[4]), "traderid": int(data[5]), "time": int(data[6]),
@@ -113,9 +144,9 @@ def process_msg(cfg, book, data):               # cond_type_side_save_bidask :68
     elif index == 1:
         bids, asks, trades = _lim(cfg, msg, bids, asks, trades, True)
     elif index == 2:
-        asks = cancel_order(cfg, asks, msg)
+        asks = cancel_order(cfg, asks, msg, key)
     elif index == 3:
-        bids = cancel_order(cfg, bids, msg)
+        bids = cancel_order(cfg, bids, msg, key)
     return asks, bids, trades
 
 
@@ -127,11 +158,13 @@ def best_quotes(cfg, asks, bids):               # :932-984
             [bb, int(bids[bids[:, 0] == bb, 1].astype(np.int64).sum())])
 
 
-def scan_save_bidask(cfg, msgs, asks, bids, trades):   # :791-823
+def scan_save_bidask(cfg, msgs, asks, bids, trades, key=(0, 0)):   # :791-823
     book = (np.array(asks, I32), np.array(bids, I32), np.array(trades, I32))
     ba, bb = [], []
-    for m in np.asarray(msgs, I32):
-        book = process_msg(cfg, book, m)
+    msgs = np.asarray(msgs, I32)
+    keys = split(key, len(msgs), cfg.get("partitionable", True)) if cfg["cancel_mode"] >= 2 else [None] * len(msgs)
+    for m, k in zip(msgs, keys):
+        book = process_msg(cfg, book, m, k)
         a, b = best_quotes(cfg, book[0], book[1])
         ba.append(a)
         bb.append(b)

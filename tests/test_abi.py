@@ -65,11 +65,11 @@ def _env_cfg(name="2_player_fq_fqc"):
 
 
 def test_error_null_and_shape(L):
-    assert L.hftlob_book_process(None, 1, 1, None, None, None, None, None, None, None) == -2
+    assert L.hftlob_book_process(None, 1, 1, None, None, None, None, None, None, None, None) == -2
     lob = pack_lob_cfg(builtin_config("2_player_fq_fqc").world_config)
-    assert L.hftlob_book_process(C.byref(lob), -1, 1, None, None, None, None, None, None, None) == -3
-    assert L.hftlob_book_process(C.byref(lob), 0, 1, None, None, None, None, None, None, None) == 0  # empty batch
-    assert L.hftlob_book_process(C.byref(lob), 4, 8, None, None, None, None, None, None, None) == -2
+    assert L.hftlob_book_process(C.byref(lob), -1, 1, None, None, None, None, None, None, None, None) == -3
+    assert L.hftlob_book_process(C.byref(lob), 0, 1, None, None, None, None, None, None, None, None) == 0  # empty batch
+    assert L.hftlob_book_process(C.byref(lob), 4, 8, None, None, None, None, None, None, None, None) == -2
     assert b"null" in L.hftlob_last_error()
     c = _env_cfg()
     out = StepOut()
@@ -82,13 +82,21 @@ def test_error_null_and_shape(L):
     assert L.hftlob_sample_actions(None, 4, None, None, None) == -2
 
 
-@pytest.mark.parametrize("field,value,code", [("cancel_mode", 2, -1), ("type_4_interpretation", 3, -1),
+@pytest.mark.parametrize("field,value,code", [("cancel_mode", 4, -1), ("type_4_interpretation", 3, -1),
                                               ("n_orders", 0, -3), ("n_trades", 257, -3)])
 def test_error_bad_lob_cfg(L, field, value, code):
     lob = pack_lob_cfg(builtin_config("2_player_fq_fqc").world_config)
     setattr(lob, field, value)
     dummy = C.c_void_p(16)  # never dereferenced: validation fails first
-    assert L.hftlob_book_process(C.byref(lob), 1, 1, dummy, dummy, dummy, dummy, None, None, None) == code
+    assert L.hftlob_book_process(C.byref(lob), 1, 1, dummy, dummy, dummy, dummy, dummy, None, None, None) == code
+
+
+def test_random_cancel_needs_keys(L):
+    lob = pack_lob_cfg(builtin_config("2_player_fq_fqc").world_config)
+    lob.cancel_mode = 2
+    dummy = C.c_void_p(16)  # never dereferenced: the NULL keys are refused first
+    assert L.hftlob_book_process(C.byref(lob), 1, 1, None, dummy, dummy, dummy, dummy, None, None, None) == -2
+    assert b"keys" in L.hftlob_last_error()
 
 
 def test_error_bad_env_cfg(L):

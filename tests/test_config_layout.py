@@ -76,8 +76,12 @@ def test_unsupported_options_fail_loudly(agent, changes, err):
         pack_env_cfg(dataclasses.replace(cfg, dict_of_agents_configs=agents), 4, 10_000, True)
 
 
-def test_cancel_mode_random_rejected():
+def test_cancel_mode_values():
     cfg = builtin_config("2_player_fq_fqc")
-    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, cancel_mode=2))
-    with pytest.raises(NotImplementedError):
+    for mode in (0, 1, 2, 3):
+        c = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, cancel_mode=mode))
+        packed, _ = pack_env_cfg(c, 4, 10_000, False)
+        assert packed.lob.cancel_mode == mode and packed.lob.prng_partitionable == 0 == packed.prng_partitionable
+    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, cancel_mode=4))
+    with pytest.raises(ValueError):
         pack_env_cfg(cfg, 4, 10_000, True)

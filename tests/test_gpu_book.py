@@ -1,4 +1,6 @@
 """Engine parity: HIP hftlob_book_process vs the CPU oracle, bit-exact (int32)."""
+import zlib
+
 import numpy as np
 import pytest
 import torch
@@ -20,17 +22,24 @@ CASES = [
     dict(nOrders=16, nTrades=8),                                # book-full eviction + trade overwrite
     dict(nOrders=40, nTrades=30, type_4_interpretation=1),
     dict(nOrders=200, nTrades=150),                             # 4 slot sets per lane
+    dict(cancel_mode=2),                                        # random cancel fallback (:141-155)
+    dict(cancel_mode=3),                                        # + random large (:157-164)
+    dict(cancel_mode=3, nOrders=40, nTrades=30, _legacy=True),  # legacy threefry split / bits
+    dict(cancel_mode=2, nOrders=200, nTrades=150),
 ]
 
 
-def _run(cfg, msgs, a0, b0, t0):
-    lc = pack_lob_cfg(cfg)
-    oa, ob, ot, oba, obb = O.book_process(lc, msgs, a0, b0, t0)
+def _run(cfg, msgs, a0, b0, t0, part=True):
+    lc = pack_lob_cfg(cfg, part)
+    E = msgs.shape[0]
+    keys = np.random.default_rng(E + msgs.shape[1]).integers(0, 2**32, (E, 2), dtype=np.uint64).astype(np.uint32)
+    oa, ob, ot, oba, obb = O.book_process(lc, msgs, a0, b0, t0, keys=keys)
     dev = "cuda"
     ga, gb, gt = (torch.from_numpy(x.copy()).to(dev) for x in (a0, b0, t0))
     gba = torch.empty((msgs.shape[0], msgs.shape[1], 2), dtype=torch.int32, device=dev)
     gbb = torch.empty_like(gba)
-    book_process_(cfg, torch.from_numpy(msgs).to(dev), ga, gb, gt, gba, gbb)
+    book_process_(cfg, torch.from_numpy(msgs).to(dev), ga, gb, gt, gba, gbb,
+                  keys=torch.from_numpy(keys.view(np.int32)).to(dev), prng_partitionable=part)
     torch.cuda.synchronize()
     for name, o, g in (("asks", oa, ga), ("bids", ob, gb), ("trades", ot, gt), ("best_asks", oba, gba),
                        ("best_bids", obb, gbb)):
@@ -41,16 +50,18 @@ def _run(cfg, msgs, a0, b0, t0):
 
 @pytest.mark.parametrize("kw", CASES, ids=[str(k) or "default" for k in CASES])
 def test_book_random_streams(kw):
+    kw = dict(kw)
+    part = not kw.pop("_legacy", False)
     cfg = JAXLOB_Configuration(**kw)
     E, M = 48, 300
     init = init_book_messages(E, seed=1)
     empty_a = np.full((E, cfg.nOrders, 6), -1, np.int32)
     empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
     a0, b0, t0, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
-    msgs = random_streams(E, M, seed=hash(str(kw)) % 1000)
-    _run(cfg, msgs, a0, b0, empty_t)
+    msgs = random_streams(E, M, seed=zlib.crc32(str(sorted(kw.items())).encode()) % 1000)
+    _run(cfg, msgs, a0, b0, empty_t, part)
     # and from empty books, with a non-empty incoming trade log
-    _run(cfg, msgs, empty_a, empty_a, t0)
+    _run(cfg, msgs, empty_a, empty_a, t0, part)
 
 
 def test_book_functional_api():

@@ -115,6 +115,14 @@ def test_env_rollout_parity(name, mid):
     rollout_parity(builtin_config(name), mid)
 
 
+@pytest.mark.parametrize("mode,part", [(2, True), (3, True), (3, False)])
+def test_env_rollout_parity_random_cancel(mode, part):
+    """cancel_mode 2/3: the engine's random cancel fallback draws from the step's scan key."""
+    cfg = builtin_config("2_player_fq_fqc")
+    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, cancel_mode=mode))
+    rollout_parity(cfg, E=32, K=66, partitionable=part)
+
+
 @pytest.mark.parametrize("name", ["2_player_fq_fqc", "3_player_fq_fqc_dir"])
 def test_env_rollout_parity_legacy_prng(name):
     """jax_threefry_partitionable=False (the pre-0.5 JAX default) split / random_bits."""

@@ -105,3 +105,40 @@ def test_c_oracle_vs_numpy_oracle_random(kw):
         (ra, rb, rt), rba, rbb = R.scan_save_bidask(rc, full[i], e6[i], e6[i], e8[i])
         assert (ra == a[i]).all() and (rb == b[i]).all() and (rt == t[i]).all()
         assert (rba == ba[i]).all() and (rbb == bb[i]).all()
+
+
+@pytest.mark.parametrize("mode,part", [(2, True), (3, True), (3, False)])
+def test_c_oracle_vs_numpy_oracle_random_cancel(mode, part):
+    """cancel_mode 2/3 (get_random_id_match / get_random_large_id_match): C vs numpy restatement."""
+    cfg = JAXLOB_Configuration(cancel_mode=mode)
+    rc = R.default_cfg(cancel_mode=mode, partitionable=part)
+    E, M = 6, 160
+    init = init_book_messages(E, seed=4)
+    msgs = random_streams(E, M, seed=21)
+    full = np.concatenate([init, msgs], axis=1)
+    e6 = np.full((E, cfg.nOrders, 6), -1, np.int32)
+    e8 = np.full((E, cfg.nTrades, 8), -1, np.int32)
+    keys = np.random.default_rng(mode).integers(0, 2**32, (E, 2), dtype=np.uint64).astype(np.uint32)
+    a, b, t, ba, bb = O.book_process(pack_lob_cfg(cfg, part), full, e6, e6, e8, keys=keys)
+    a1, b1, _, _, _ = O.book_process(pack_lob_cfg(JAXLOB_Configuration(cancel_mode=1)), full, e6, e6, e8)
+    assert (a1 != a).any() or (b1 != b).any(), "the random fallback never changed the book"
+    for i in range(E):
+        (ra, rb, rt), rba, rbb = R.scan_save_bidask(rc, full[i], e6[i], e6[i], e8[i], key=tuple(int(x) for x in keys[i]))
+        assert (ra == a[i]).all() and (rb == b[i]).all() and (rt == t[i]).all()
+        assert (rba == ba[i]).all() and (rbb == bb[i]).all()
+
+
+def test_random_cancel_choice_semantics():
+    """Hand-derived: with one price-matched order the draw must pick it, whatever the key;
+    with none, chosen id is 0 and the -1 index wraps to the last slot."""
+    cfg = R.default_cfg(cancel_mode=2, nOrders=4)
+    side = np.full((4, 6), -1, np.int32)
+    side[0] = [100, 5, 77, 1, 0, 0]
+    side[2] = [101, 9, 55, 1, 0, 0]
+    msg = dict(price=101, quantity=3, orderid=999)
+    for k in range(20):
+        assert R.get_random_id_match(cfg, (k, 3 * k + 1), side, msg) == 2
+    msg = dict(price=102, quantity=3, orderid=999)
+    assert R.get_random_id_match(cfg, (1, 2), side, msg) == -1
+    out = R.cancel_order(cfg, side, msg, key=(1, 2))
+    assert (out[3] == -1).all() and (out[:3] == side[:3]).all()   # slot -1 (empty) -> stays removed
