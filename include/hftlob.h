@@ -159,7 +159,8 @@ typedef struct hftlob_env_cfg {
     int32_t n_action_msgs;         /* A = sum_t n_agents_t * n_action_msgs_t */
     int32_t n_cancel_msgs;         /* C = M - D - A */
     int32_t tick_size;
-    int32_t ep_type;               /* 0 fixed_steps (1 fixed_time unsupported) */
+    int32_t ep_type;               /* 0 fixed_steps, 1 fixed_time (data rows past init_time[0] +
+                                      episode_time are masked; EXE engineered obs has 15 fields) */
     int32_t episode_time;
     int32_t window_selector;       /* -1 random */
     int32_t n_windows;

@@ -991,6 +991,9 @@ struct Obs {
 struct WorldView {  // wave-uniform world quantities used by obs
     i32 best_ask_p, best_bid_p, vol_a, vol_b, step, max_steps;
     float mid;
+    // fixed_time episodes (EXE engineered obs): world time, init_time, delta_time
+    i32 t0, t1, it0, it1;
+    float dt;
 };
 
 // MM _get_obs_basic / _get_obs_engineered (fixed_steps), sorted keys — mm_env.py:2963-3154
@@ -1012,7 +1015,9 @@ DEV void mm_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* 
     o[7] = nz ? i2f(w.step) / 10.0f : i2f(w.step);
 }
 // EXE _get_obs (fixed_steps), sorted keys — exec_env.py:1913-2079
-DEV void exe_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o) {
+// ftime: ep_type == fixed_time, passed by the caller (compile-time false in the 100/100 kernel)
+DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o,
+                 bool ftime) {
     const bool nz = tc.normalize;
     const i32 sell = st[3];
     const i32 p_aggr = sell ? w.best_bid_p : w.best_ask_p, p_pass = sell ? w.best_ask_p : w.best_bid_p;
@@ -1020,6 +1025,37 @@ DEV void exe_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32*
     const float ip = bitf(st[0]);
     const float ts = (float)tc.task_size;
     const float rr = w.max_steps == 0 ? 0.0f : 1.0f - i2f(w.step) / i2f(w.max_steps);
+    if (ftime) {
+        // fixed_time (exec_env.py:1940-2010): 15 keys, sorted: delta_time, executed_quant, init_price,
+        // is_sell_task, p_aggr, p_pass, q_aggr, q_pass, remaining_quant, remaining_ratio, spread,
+        // step_counter, task_size, time, time_remaining
+        const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
+        const float te = tm - (i2f(w.it0) + i2f(w.it1) / 1e9f);
+        const float trem = (float)c.episode_time - te;
+        if (nz) {
+            o[0] = w.dt / 10.0f;
+            o[1] = i2f(st[2]) / ts;
+            o[2] = ip / 1e7f;
+            o[3] = i2f(sell) / 1.0f;
+            o[4] = (i2f(p_aggr) - ip) / 1e5f;
+            o[5] = (i2f(p_pass) - ip) / 1e5f;
+            o[6] = i2f(q_aggr) / 1000.0f;
+            o[7] = i2f(q_pass) / 1000.0f;
+            o[8] = i2f(wsub(st[1], st[2])) / ts;
+            o[9] = rr / 1.0f;
+            o[10] = i2f(iabs_(wsub(p_aggr, p_pass))) / 1e4f;
+            o[11] = i2f(w.step) / 30.0f;
+            o[12] = i2f(st[1]) / ts;
+            o[13] = tm / 1e5f;
+            o[14] = trem / (float)c.episode_time;
+        } else {
+            o[0] = w.dt; o[1] = i2f(st[2]); o[2] = ip; o[3] = i2f(sell); o[4] = i2f(p_aggr); o[5] = i2f(p_pass);
+            o[6] = i2f(q_aggr); o[7] = i2f(q_pass); o[8] = i2f(wsub(st[1], st[2])); o[9] = rr;
+            o[10] = i2f(iabs_(wsub(p_aggr, p_pass))); o[11] = i2f(w.step); o[12] = i2f(st[1]); o[13] = tm;
+            o[14] = trem;
+        }
+        return;
+    }
     if (nz) {
         o[0] = i2f(st[2]) / ts;
         o[1] = ip / 1e7f;
@@ -1041,12 +1077,12 @@ DEV void exe_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32*
 }
 // write one agent's obs row (lanes 0..obs_stride-1 store one float each)
 DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st,
-                   float* dst, bool zero) {
+                   float* dst, bool zero, bool ftime) {
     float o[HFTLOB_MAX_OBS];
 #pragma unroll
     for (int k = 0; k < HFTLOB_MAX_OBS; ++k) o[k] = 0.0f;
     if (tc.kind == HFTLOB_AGENT_MM) mm_obs(tc, w, st, o);
-    else exe_obs(tc, w, st, o);
+    else exe_obs(c, tc, w, st, o, ftime);
     const int l = lane_id();
     float v = 0.0f;
 #pragma unroll
@@ -1060,7 +1096,7 @@ DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
 // mm_env.py:417-459, exec_env.py:209-266.  Writes the whole record + obs.
 template <int S>
 DEV void env_reset_dev(const hftlob_env_cfg& c, Key key, const i32* __restrict__ init_states, i32* __restrict__ rec,
-                       float* __restrict__ obs, const Valid<S>& VS, const Valid<S>& VT) {
+                       float* __restrict__ obs, const Valid<S>& VS, const Valid<S>& VT, bool ftime) {
     const bool part = c.prng_partitionable;
     const int nTy = c.n_types, l = lane_id();
     Key wk = split_key(key, nTy + 1, nTy, part);
@@ -1095,6 +1131,7 @@ DEV void env_reset_dev(const hftlob_env_cfg& c, Key key, const i32* __restrict__
     wv.best_ask_p = ba_p; wv.best_bid_p = bb_p;
     wv.vol_a = side_volume_pq(ap, aq, VS); wv.vol_b = side_volume_pq(bp, bq, VS);
     wv.step = src[c.off_loaded + LD_STEP]; wv.max_steps = src[c.off_loaded + LD_MAXS]; wv.mid = mid;
+    wv.t0 = wv.it0 = t0; wv.t1 = wv.it1 = t1; wv.dt = 0.0f;  // world time = init_time, delta_time 0
     // zero the record's padding words (after the world block, after the agents)
     int agents_end = c.off_agents;
     for (int t = 0; t < nTy; ++t) agents_end += c.types[t].n_agents * agent_words(c.types[t]);
@@ -1119,7 +1156,7 @@ DEV void env_reset_dev(const hftlob_env_cfg& c, Key key, const i32* __restrict__
             i32 v = 0;
             for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
             if (l < nw) st[l] = v;
-            if (obs) write_obs(c, tc, wv, s, obs + (size_t)ag * c.obs_stride, false);
+            if (obs) write_obs(c, tc, wv, s, obs + (size_t)ag * c.obs_stride, false, ftime);
             st += nw;
         }
     }
@@ -1136,7 +1173,7 @@ __global__ __launch_bounds__(64) void k_env_reset(hftlob_env_cfg c, int n_env, c
     VT.init(c.lob.n_trades);
     Key k{keys[2 * e], keys[2 * e + 1]};
     env_reset_dev<S>(c, k, init_states, state + (size_t)e * c.rec_words,
-                     obs ? obs + (size_t)e * c.n_agents * c.obs_stride : nullptr, VS, VT);
+                     obs ? obs + (size_t)e * c.n_agents * c.obs_stride : nullptr, VS, VT, c.ep_type == 1);
 }
 
 // ------------------------------------------------------------ agent logic
@@ -1668,6 +1705,16 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     return o;
 }
 
+// BaseLOBEnv.get_data_messages, fixed_time (base_env.py:358-367): a data row
+// whose time_s >= the episode end time becomes [0 x 6, time_s, time_ns]
+DEV void fixed_time_mask(int4& x, int4& y, i32 t_end) {
+    if (y.z >= t_end) {
+        x = make_int4(0, 0, 0, 0);
+        y.x = 0;
+        y.y = 0;
+    }
+}
+
 // ====================================================== K2: fused env step
 // MARLEnv.step — marl_env.py:775-804 (step_env :211-709, auto-reset select)
 #define MAX_AGENT_ROWS 128
@@ -1735,11 +1782,15 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     // first chunk is fetched now, ahead of the agent phase
     i32 dstart = wadd(start_index, wmul(D, step));
     dstart = imax_(0, imin_(dstart, c.n_data_rows - D));  // dynamic_slice clamping
+    // fixed_time: rows at or after init_time[0] + episode_time keep only their time (base_env.py:358-367)
+    const bool ftime = NFIX == 0 && c.ep_type == 1;  // the 100/100 kernel is launched for fixed_steps only
+    const i32 t_end = wadd(ld_t0, c.episode_time);
     int4 px = make_int4(0, 0, 0, 0), py = px;
     if ((l >= C + A) & (l < M)) {
         const i32* g = msg_data + (size_t)(dstart + l - (C + A)) * 8;
         px = reinterpret_cast<const int4*>(g)[0];
         py = reinterpret_cast<const int4*>(g)[1];
+        if (ftime) fixed_time_mask(px, py, t_end);
     }
     B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs);
     B.fl |= fast_bit(B.fl);
@@ -1853,6 +1904,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
             const i32* g = msg_data + (size_t)(dstart + row - AR) * 8;
             x = reinterpret_cast<const int4*>(g)[0];
             y = reinterpret_cast<const int4*>(g)[1];
+            if (ftime) fixed_time_mask(x, y, t_end);
         }
         decode_msgs(B.c, x, y);
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
@@ -1912,6 +1964,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     store_side(B.b, rec + c.off_bids, R, B.vs);
     store_trades(B.tr, rec + c.off_trades, B.vt);
     wv.step = wadd(step, 1); wv.max_steps = max_steps; wv.mid = X.last_mid;
+    wv.t0 = last_t0; wv.t1 = last_t1; wv.it0 = ld_t0; wv.it1 = Lr[LD_T1];
+    const float dt = i2f(last_t0) + i2f(last_t1) / 1e9f - i2f(wt0) - i2f(wt1) / 1e9f;  // marl_env.py:496
+    wv.dt = dt;
     i32* info = info_out ? info_out + (size_t)e * c.info_words : nullptr;
     {
         int ag = 0;
@@ -1976,7 +2031,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                     i32 v = 0;
                     for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
                     if (l < nw) st[l] = v;
-                    write_obs(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0);
+                    write_obs(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0, ftime);
                 }
                 st += nw;
             }
@@ -1985,7 +2040,6 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     STAMP(t_rewards);
     // ---- (F) world state + info
     const float new_mid = X.last_mid;
-    const float dt = i2f(last_t0) + i2f(last_t1) / 1e9f - i2f(wt0) - i2f(wt1) / 1e9f;
     if (info) {
         const float ava = wave_fsum(pa_acc) / (float)M, avb = wave_fsum(pb_acc) / (float)M;
         i32 wv_[HFTLOB_INFO_WORLD_WORDS] = {win, fbit(new_mid), wadd(step, 1), last_t0, last_t1, wsub(oidc, A),
@@ -2007,7 +2061,8 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     }
 #endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
-        env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt);
+        env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt,
+                         ftime);
         return;
     }
     if (l == 0) {
@@ -2101,7 +2156,7 @@ static int check_env(const hftlob_env_cfg* c) {
     if (!c) return fail(HFTLOB_ENULL, "null cfg");
     int rc = check_lob(&c->lob);
     if (rc) return rc;
-    if (c->ep_type != 0) return fail(HFTLOB_EINVAL, "only ep_type fixed_steps is supported");
+    if (c->ep_type != 0 && c->ep_type != 1) return fail(HFTLOB_EINVAL, "ep_type must be 0 fixed_steps / 1 fixed_time");
     if (c->lob.prng_partitionable != c->prng_partitionable) return fail(HFTLOB_EINVAL, "lob.prng_partitionable differs");
     if (c->n_types < 1 || c->n_types > HFTLOB_MAX_TYPES || c->n_agents < 1 || c->n_agents > HFTLOB_MAX_AGENTS)
         return fail(HFTLOB_ESHAPE, "agent counts out of range");
@@ -2160,7 +2215,7 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, const uint32_t*
         if (S == 1) LAUNCH_STEP(1, 0, true);
         else if (S == 2) LAUNCH_STEP(2, 0, true);
         else LAUNCH_STEP(4, 0, true);
-    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100) LAUNCH_STEP(2, 100, false);
+    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0) LAUNCH_STEP(2, 100, false);
     else if (S == 1) LAUNCH_STEP(1, 0, false);
     else if (S == 2) LAUNCH_STEP(2, 0, false);
     else LAUNCH_STEP(4, 0, false);

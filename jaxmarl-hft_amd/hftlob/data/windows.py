@@ -41,9 +41,14 @@ def fixed_steps_windows(n_msgs: int, n_data_msg_per_step: int, episode_time: int
 
 
 def make_windows(day, world_cfg) -> Windows:
-    """Window table for a generated / loaded day (``day.books`` at ``day.snap_idx``)."""
+    """Window table for a generated day (``day.books`` at ``day.snap_idx``, fixed_steps) or a
+    ``LoadedDay`` from the LOBSTER loader (its own starts / ends / books, either episode type)."""
+    if hasattr(day, "starts"):                      # hftlob.data.lobster.LoadedDay
+        return Windows(starts=day.starts.astype(np.int32), ends=day.ends.astype(np.int32),
+                       max_msgs=day.max_msgs.astype(np.int32), books=day.books.astype(np.int32))
     if world_cfg.ep_type != "fixed_steps":
-        raise NotImplementedError("fixed_time windows are the next tier (time-masked data slices)")
+        raise ValueError("synthetic LobsterDay windows are fixed_steps; load fixed_time windows with "
+                         "hftlob.data.lobster (LoadLOBSTER_resample)")
     D = world_cfg.n_data_msg_per_step
     starts = fixed_steps_windows(day.msgs.shape[0], D, world_cfg.episode_time, world_cfg.start_resolution)
     snap_of = {int(s): k for k, s in enumerate(day.snap_idx)}
@@ -73,8 +78,20 @@ def init_messages(books: np.ndarray, first_times: np.ndarray, depth: int, init_i
     return m
 
 
+def init_times(first_times: np.ndarray, world_cfg) -> np.ndarray:
+    """LoadedEnvState.init_time (base_env.py:287-291): the window's first message time for
+    fixed_steps; for fixed_time ``[(w * res) % (day_end - day_start - episode_time + res) + day_start, 0]``."""
+    w = world_cfg
+    if getattr(w, "ep_type", "fixed_steps") != "fixed_time":
+        return first_times.astype(np.int32)
+    W = first_times.shape[0]
+    res = w.start_resolution
+    t0 = (np.arange(W, dtype=np.int64) * res) % (w.day_end - w.day_start - w.episode_time + res) + w.day_start
+    return np.stack([t0, np.zeros(W, np.int64)], 1).astype(np.int32)
+
+
 def loaded_rows(asks: np.ndarray, bids: np.ndarray, trades: np.ndarray, first_times: np.ndarray, win: Windows,
-                n_data_msg_per_step: int, init_rec_words: int) -> np.ndarray:
+                n_data_msg_per_step: int, init_rec_words: int, world_cfg=None) -> np.ndarray:
     """(W, init_rec_words) int32 LoadedEnvState rows in the record layout."""
     W, nO = asks.shape[0], asks.shape[1]
     nT = trades.shape[1]
@@ -83,8 +100,9 @@ def loaded_rows(asks: np.ndarray, bids: np.ndarray, trades: np.ndarray, first_ti
     rows[:, 6 * nO:12 * nO] = bids.reshape(W, -1)
     rows[:, 12 * nO:12 * nO + 8 * nT] = trades.reshape(W, -1)
     o = 12 * nO + 8 * nT
-    rows[:, o + 0] = first_times[:, 0]
-    rows[:, o + 1] = first_times[:, 1]
+    it = init_times(first_times, world_cfg) if world_cfg is not None else first_times
+    rows[:, o + 0] = it[:, 0]
+    rows[:, o + 1] = it[:, 1]
     rows[:, o + 2] = np.arange(W)
     rows[:, o + 3] = win.max_msgs // n_data_msg_per_step + 1
     rows[:, o + 4] = win.starts

@@ -143,9 +143,13 @@ class MultiAgentState:               # StatesandParams.py:43-47
 
 # -------------------------------------------------------------------- env
 class MARLEnv:
-    def __init__(self, key, multi_agent_config: MultiAgentConfig, data: Optional[LobsterDay] = None,
+    def __init__(self, key, multi_agent_config: MultiAgentConfig, data=None,
                  device=None, prng_partitionable: bool = True, return_info: bool = True,
                  persistent_outputs: bool = False):
+        """data: a synthetic ``LobsterDay`` (None = the seeded default day), a ``LoadedDay`` from
+        ``hftlob.data.lobster``, or ``"lobster"`` to load ``world_config.dataPath`` /
+        ``stock`` / ``timePeriod`` through ``LoadLOBSTER_resample`` as the reference's
+        ``BaseLOBEnv.__init__`` does (base_env.py:157-176)."""
         self.multi_agent_config = cfg = multi_agent_config
         self.device = torch.device(device or "cuda")
         w = cfg.world_config
@@ -154,6 +158,11 @@ class MARLEnv:
         self.type_names = [a.short_name for a in self.list_of_agents_configs]
         if data is None:
             data = generate_day(seed=20260403, snap_every=w.n_data_msg_per_step * w.start_resolution)
+        elif isinstance(data, str):
+            if data != "lobster":
+                raise ValueError(f"data={data!r}: pass a LobsterDay, a LoadedDay or 'lobster'")
+            from .data.lobster import load_from_config
+            data = load_from_config(w)
         self.data = data
         self.windows: Windows = make_windows(data, w)
         self.n_windows = len(self.windows.starts)
@@ -184,7 +193,7 @@ class MARLEnv:
         keys = torch.zeros((W, 2), dtype=torch.int32, device=dev)
         book_process_(w, im.contiguous(), asks, bids, trades, keys=keys, prng_partitionable=self.prng_partitionable)
         rows = loaded_rows(asks.cpu().numpy(), bids.cpu().numpy(), trades.cpu().numpy(), first_times,
-                           self.windows, w.n_data_msg_per_step, L.init_rec_words)
+                           self.windows, w.n_data_msg_per_step, L.init_rec_words, w)
         return torch.from_numpy(rows).to(dev)
 
     @property

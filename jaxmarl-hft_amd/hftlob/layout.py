@@ -106,12 +106,17 @@ def _r4(x: int) -> int:
     return (x + 3) // 4 * 4
 
 
+EP_TYPE = {"fixed_steps": 0, "fixed_time": 1}
+
+
 def obs_dim(agent_cfg, world) -> int:
-    if world.ep_type != "fixed_steps":
-        raise NotImplementedError("only ep_type='fixed_steps' is implemented (fixed_time: next tier)")
+    """observation_space() widths: mm_env.py (basic 2, engineered 8, both episode types);
+    exec_env.py:2185-2200 (engineered: 12 fixed_steps, 15 fixed_time)."""
+    if world.ep_type not in EP_TYPE:
+        raise ValueError(f"ep_type {world.ep_type!r}: use 'fixed_steps' or 'fixed_time'")
     if isinstance(agent_cfg, MarketMaking_EnvironmentConfig):
         return {"basic": 2, "engineered": 8}[agent_cfg.observation_space]
-    return {"engineered": 12}[agent_cfg.observation_space]
+    return {"engineered": 12 if world.ep_type == "fixed_steps" else 15}[agent_cfg.observation_space]
 
 
 @dataclass
@@ -260,7 +265,7 @@ def pack_env_cfg(cfg: MultiAgentConfig, n_windows: int, n_data_rows: int,
     c = EnvCfg()
     c.lob = pack_lob_cfg(w, prng_partitionable)
     c.n_data_msg, c.n_msgs, c.n_action_msgs, c.n_cancel_msgs = L.n_data_msg, L.n_msgs, L.n_action_msgs, L.n_cancel_msgs
-    c.tick_size, c.ep_type, c.episode_time = w.tick_size, 0, w.episode_time
+    c.tick_size, c.ep_type, c.episode_time = w.tick_size, EP_TYPE[w.ep_type], w.episode_time
     c.window_selector, c.n_windows, c.n_data_rows = w.window_selector, n_windows, n_data_rows
     c.placeholder_order_id = w.placeholder_order_id
     c.artificial_trader_id, c.artificial_order_id = w.artificial_trader_id_end_episode, w.artificial_order_id_end_episode

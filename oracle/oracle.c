@@ -930,7 +930,7 @@ static void mm_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env
     o[7] = nrm(i2f(LOADED(E)[5]), 10.0f, nz);
 }
 
-/* EXE _get_obs (fixed_steps) — exec_env.py:1913-2079; sorted keys */
+/* EXE _get_obs — exec_env.py:1913-2079; sorted keys (fixed_steps 12, fixed_time 15) */
 static void exe_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env* E, const i32* st, float* o) {
     int M = c->n_msgs, nO = c->lob.n_orders, nz = tc->normalize;
     i32 sell = st[3];
@@ -942,6 +942,39 @@ static void exe_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, En
     float ts = (float)tc->task_size;
     i32 ms = LOADED(E)[3], sc = LOADED(E)[5];
     float rr = ms == 0 ? 0.0f : 1.0f - i2f(sc) / i2f(ms);
+    if (c->ep_type == 1) {
+        /* fixed_time (exec_env.py:1940-2010), 15 sorted keys: delta_time, executed_quant, init_price,
+         * is_sell_task, p_aggr, p_pass, q_aggr, q_pass, remaining_quant, remaining_ratio, spread,
+         * step_counter, task_size, time, time_remaining.  time = t[0] + t[1]/1e9 (f32). */
+        const i32* W = WORLD(E);
+        const i32* L = LOADED(E);
+        float tm = i2f(W[0]) + i2f(W[1]) / 1e9f;
+        float te = tm - (i2f(L[0]) + i2f(L[1]) / 1e9f);
+        float trem = (float)c->episode_time - te;
+        float dt = bitf(W[4]);
+        float v[15] = {dt, i2f(st[2]), ip, i2f(sell), i2f(p_aggr), i2f(p_pass), i2f(q_aggr), i2f(q_pass),
+                       i2f(wsub(st[1], st[2])), rr, i2f(iabs(wsub(p_aggr, p_pass))), i2f(sc), i2f(st[1]), tm, trem};
+        if (nz) {
+            o[0] = dt / 10.0f;
+            o[1] = i2f(st[2]) / ts;
+            o[2] = ip / 1e7f;
+            o[3] = i2f(sell) / 1.0f;
+            o[4] = (i2f(p_aggr) - ip) / 1e5f;
+            o[5] = (i2f(p_pass) - ip) / 1e5f;
+            o[6] = i2f(q_aggr) / 1000.0f;
+            o[7] = i2f(q_pass) / 1000.0f;
+            o[8] = i2f(wsub(st[1], st[2])) / ts;
+            o[9] = rr / 1.0f;
+            o[10] = i2f(iabs(wsub(p_aggr, p_pass))) / 1e4f;
+            o[11] = i2f(sc) / 30.0f;
+            o[12] = i2f(st[1]) / ts;
+            o[13] = tm / 1e5f;
+            o[14] = trem / (float)c->episode_time;
+        } else {
+            for (int k = 0; k < 15; ++k) o[k] = v[k];
+        }
+        return;
+    }
     if (nz) {
         o[0] = i2f(st[2]) / ts;
         o[1] = ip / 1e7f;
@@ -1013,7 +1046,7 @@ static void env_reset_one(const hftlob_env_cfg* c, const u32* key, const i32* in
 
 static int env_cfg_ok(const hftlob_env_cfg* c) {
     if (!lob_cfg_ok(&c->lob)) return 0;
-    if (c->ep_type != 0 || c->n_types < 1 || c->n_types > HFTLOB_MAX_TYPES) return 0;
+    if ((c->ep_type != 0 && c->ep_type != 1) || c->n_types < 1 || c->n_types > HFTLOB_MAX_TYPES) return 0;
     if (c->n_msgs > HFTLOB_MAX_MSGS || c->n_agents > HFTLOB_MAX_AGENTS || c->n_windows < 1) return 0;
     if (c->obs_stride > HFTLOB_MAX_OBS) return 0;
     for (int t = 0; t < c->n_types; ++t) {
@@ -1051,6 +1084,13 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     if (start > c->n_data_rows - D) start = c->n_data_rows - D;
     i32 comb[HFTLOB_MAX_MSGS * 8];
     memcpy(comb + (size_t)(C + A) * 8, msg_data + (size_t)start * 8, (size_t)D * 8 * sizeof(i32));
+    if (c->ep_type == 1) { /* fixed_time: rows past init_time[0] + episode_time keep only their time (base_env.py:358-367) */
+        i32 t_end = wadd(L[0], c->episode_time);
+        for (int r = 0; r < D; ++r) {
+            i32* row = comb + (size_t)(C + A + r) * 8;
+            if (row[6] >= t_end) memset(row, 0, 6 * sizeof(i32));
+        }
+    }
     /* (C) agent messages */
     i32 actm[HFTLOB_MAX_MSGS * 8], cnlm[HFTLOB_MAX_MSGS * 8];
     ActX ax[HFTLOB_MAX_AGENTS];

@@ -148,4 +148,4 @@ def init_states(env_cfg_lob, windows, msgs, world_cfg, init_rec_words):
     a0 = np.full((W, world_cfg.nOrders, 6), -1, np.int32)
     t0 = np.full((W, world_cfg.nTrades, 8), -1, np.int32)
     a, b, t, _, _ = book_process(env_cfg_lob, im, a0, a0, t0, save_best=False)
-    return loaded_rows(a, b, t, ft, windows, world_cfg.n_data_msg_per_step, init_rec_words)
+    return loaded_rows(a, b, t, ft, windows, world_cfg.n_data_msg_per_step, init_rec_words, world_cfg)

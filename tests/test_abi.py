@@ -102,7 +102,7 @@ def test_random_cancel_needs_keys(L):
 def test_error_bad_env_cfg(L):
     dummy = C.c_void_p(16)
     out = StepOut(16, 16, 16, 16, None)
-    for mutate, code in ((lambda c: setattr(c, "ep_type", 1), -1),
+    for mutate, code in ((lambda c: setattr(c, "ep_type", 2), -1),
                          (lambda c: setattr(c, "n_agents", 3), -1),
                          (lambda c: setattr(c, "n_msgs", 1000), -3),
                          (lambda c: setattr(c.types[0], "kind", 7), -1),

@@ -68,9 +68,9 @@ def _day(w, mid, seed=11):
     return _DAYS[key]
 
 
-def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True):
+def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True, day=None):
     w = cfg.world_config
-    day = _day(w, mid, seed)
+    day = _day(w, mid, seed) if day is None else day
     env = MARLEnv(None, cfg, data=day, prng_partitionable=partitionable)
     params = env.default_params
     init = O.init_states(env.cfg_c.lob, env.windows, day.msgs, w, env.layout.init_rec_words)
@@ -113,6 +113,41 @@ def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True):
                                       ("exec_debug_fixed_quants_complex", 2_000_000)])
 def test_env_rollout_parity(name, mid):
     rollout_parity(builtin_config(name), mid)
+
+
+_LOADED = {}
+
+
+def _loaded(ep_type, tmp_root):
+    """A generated raw LOBSTER day through hftlob.data.lobster (LoadLOBSTER_resample)."""
+    from hftlob.data import lobster as Lb
+    from hftlob.data.raw_synthetic import write_raw_lobster_day
+    if "root" not in _LOADED:
+        write_raw_lobster_day(tmp_root, n_events=30_000, seed=5, mid=2_000_000)
+        _LOADED["root"] = tmp_root
+    root = _LOADED["root"]
+    if ep_type == "fixed_steps":
+        ld = Lb.LoadLOBSTER_resample(root, root, 10, "fixed_steps", window_length=64, window_resolution=16,
+                                     n_data_msg_per_step=100, stock="SYN", time_period="2026_Oct")
+        return Lb.LoadedDay.from_arrays(*ld.run_loading("gpu_fs"))
+    ld = Lb.LoadLOBSTER_resample(root, root, 10, "fixed_time", window_length=300, window_resolution=300,
+                                 n_data_msg_per_step=100, stock="SYN", time_period="2026_Oct")
+    return Lb.LoadedDay.from_arrays(*ld.run_loading("gpu_ft"))
+
+
+@pytest.mark.parametrize("ep_type", ["fixed_steps", "fixed_time"])
+def test_env_rollout_parity_lobster_loaded(ep_type, tmp_path_factory):
+    """Raw LOBSTER files -> loader -> env: fixed_steps windows, and fixed_time windows with the
+    data-row time mask (base_env.py:358-367) and the 15-field EXE obs (exec_env.py:1940-2010)."""
+    day = _loaded(ep_type, str(tmp_path_factory.mktemp("lob")))
+    cfg = builtin_config("2_player_fq_fqc")
+    w = dataclasses.replace(cfg.world_config, ep_type=ep_type,
+                            episode_time=64 if ep_type == "fixed_steps" else 300,
+                            start_resolution=16 if ep_type == "fixed_steps" else 300)
+    cfg = dataclasses.replace(cfg, world_config=w)
+    rollout_parity(cfg, E=32, K=40, day=day)
+    for norm in (False,):
+        rollout_parity(variant(cfg, "Execution", normalize=norm), E=16, K=12, day=day)
 
 
 @pytest.mark.parametrize("mode,part", [(2, True), (3, True), (3, False)])
