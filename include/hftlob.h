@@ -65,7 +65,9 @@ typedef struct hftlob_lob_cfg {
 
 /* ---- agent kinds and the option enums (jaxen/mm_env.py, jaxen/exec_env.py) */
 enum { HFTLOB_AGENT_MM = 0, HFTLOB_AGENT_EXE = 1 };
-enum { HFTLOB_MM_ACT_FIXED_QUANTS = 0, HFTLOB_MM_ACT_DIRECTIONAL = 1 };
+enum { HFTLOB_MM_ACT_FIXED_QUANTS = 0, HFTLOB_MM_ACT_DIRECTIONAL = 1, HFTLOB_MM_ACT_BOB_RL = 2,
+       HFTLOB_MM_ACT_BOB_STRATEGY = 3, HFTLOB_MM_ACT_AVST = 4, HFTLOB_MM_ACT_SPREAD_SKEW = 5,
+       HFTLOB_MM_ACT_SIMPLE = 6 };
 enum { HFTLOB_MM_OBS_BASIC = 0, HFTLOB_MM_OBS_ENGINEERED = 1 };
 enum { HFTLOB_MM_REW_PORTFOLIO_VALUE = 0, HFTLOB_MM_REW_BUY_SELL_PNL, HFTLOB_MM_REW_COMPLEX,
        HFTLOB_MM_REW_ZERO_INV, HFTLOB_MM_REW_SPOONER, HFTLOB_MM_REW_SPOONER_DAMPED,
@@ -126,7 +128,20 @@ typedef struct hftlob_agent_type_cfg {
     /* constants the reference forms in Python double, then uses as weak f32 */
     float   rebate_factor;         /* rebate_bps / 10_000 */
     float   one_minus_eta;         /* 1 - inventoryPnL_eta */
-    int32_t _pad;
+    /* market-maker action-space parameters (mm_env.py:1123-1809) */
+    int32_t bob_v0;                /* bobRL / bobStrategy base quantity */
+    int32_t n_ticks_offset;        /* simple */
+    int32_t simple_nothing_action; /* simple: 4-entry tables (else 3) */
+    int32_t multiplier_type;       /* spread_skew: 0 "tick", 1 "spread" */
+    float   spread_multiplier;     /* spread_skew */
+    float   skew_multiplier;       /* spread_skew */
+    float   avst_var;              /* AvSt avst_var_parameter */
+    float   avst_k;                /* AvSt avst_k_parameter */
+    float   avst_log_term[8];      /* AvSt: f32 log(1 + gamma_a / k) per action (host, correctly rounded) */
+    /* execution: doom_price_penalty * tick_size when the config gives a non-integer penalty
+       (a Python float: the far-touch price is then computed in f32, exec_env.py:1544,1569-1573) */
+    int32_t doom_penalty_is_float;
+    float   doom_penalty_f32;
 } hftlob_agent_type_cfg;
 
 /*

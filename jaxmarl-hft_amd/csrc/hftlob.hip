@@ -1258,12 +1258,12 @@ DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
 }
 
 // MM _getActionMsgs_fixedQuant — mm_env.py:970-1118
+// best ask / bid of the book with the agent's own orders masked out (get_best_bid_and_ask
+// over the masked sides, mm_env.py:979-997), floored to the tick; an empty side falls back
+// to the last recorded best quotes.  Returns empty_book.
 template <int S>
-DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, Book<S>& B, const i32* st, i32 tid,
-                        i32 action, i32 wt0, i32 wt1, i32 last_ba, i32 last_bb, i32* lds_rows, int row, ActX& x) {
-    if (tc.fixed_action_setting) action = tc.fixed_action;
+DEV bool masked_best(const hftlob_env_cfg& c, Book<S>& B, i32 tid, i32 last_ba, i32 last_bb, i32& ba, i32& bb) {
     const i32 tick = c.tick_size;
-    // best ask / bid of the book with the agent's own orders masked out
     i32 mn = INT_MAX, mx = INT_MIN, ap_[S], at_[S], bp_[S], bt_[S];
     ldcol(B.a.t, B.c.nO, FP, ap_); ldcol(B.a.t, B.c.nO, FTID, at_);
     ldcol(B.b.t, B.c.nO, FP, bp_); ldcol(B.b.t, B.c.nO, FTID, bt_);
@@ -1274,12 +1274,22 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
         mn = imin_(mn, B.vs.v[r] ? (pa == -1 ? c.lob.maxint : pa) : INT_MAX);
         mx = imax_(mx, B.vs.v[r] ? pb : INT_MIN);
     }
-    i32 ba = wave_min(mn), bb = wave_max(mx);
+    ba = wave_min(mn);
+    bb = wave_max(mx);
     ba = ba == c.lob.maxint ? -1 : ba;
     const bool empty = (ba == -1) || (bb == -1);
     ba = wmul(ifloordiv(ba, tick), tick);
     bb = wmul(ifloordiv(bb, tick), tick);
     if (empty) { bb = last_bb; ba = last_ba; }
+    return empty;
+}
+template <int S>
+DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, Book<S>& B, const i32* st, i32 tid,
+                        i32 action, i32 wt0, i32 wt1, i32 last_ba, i32 last_bb, i32* lds_rows, int row, ActX& x) {
+    if (tc.fixed_action_setting) action = tc.fixed_action;
+    const i32 tick = c.tick_size;
+    i32 ba, bb;
+    const bool empty = masked_best(c, B, tid, last_ba, last_bb, ba, bb);
     const float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
     const float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
     const int ai = action < 0 ? 0 : (action > 9 ? 9 : action);
@@ -1305,6 +1315,101 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
     put_row(lds_rows, row, typ0, sd0, qq0, pp0, c.placeholder_order_id, tid, ta, tb);
     put_row(lds_rows, row + 1, typ1, sd1, qq1, pp1, c.placeholder_order_id, tid, ta, tb);
     x.bid_price = bp; x.ask_price = ap; x.bid_dist = wsub(bb, bp); x.ask_dist = wsub(ap, ba);
+    x.bid_quant = bq; x.ask_quant = aq;
+}
+
+// MM actions bobRL / bobStrategy / AvSt / spread_skew / simple (mm_env.py:1123-1809)
+DEV i32 f2i_sat(float f) {  // XLA f32 -> s32 convert: saturating, NaN -> 0
+    return f != f ? 0 : (f >= 2147483648.0f ? INT_MAX : (f <= -2147483648.0f ? INT_MIN : (i32)f));
+}
+template <int S>
+DEV void mm_other_actions(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, Book<S>& B, const i32* st, i32 tid,
+                          i32 action, i32 wt0, i32 wt1, i32 last_ba, i32 last_bb, i32 step, i32 init_t0, i32* lds_rows,
+                          int row, ActX& x) {
+    if (tc.fixed_action_setting) action = tc.fixed_action;
+    const i32 tick = c.tick_size, inv = st[2], fq = tc.fixed_quant_value;
+    const int kind = tc.action_space;
+    // length of the indexed table: bobRL 2*v0+1, AvSt 8, simple 4 (3 without the do-nothing entry)
+    const int na = kind == HFTLOB_MM_ACT_SIMPLE ? (tc.simple_nothing_action ? 4 : 3)
+                                                 : (kind == HFTLOB_MM_ACT_AVST ? 8 : 2 * tc.bob_v0 + 1);
+    // jnp gather index: negative wraps once, then clamps into range
+    int ai = action < 0 ? action + na : action;
+    ai = ai < 0 ? 0 : (ai >= na ? na - 1 : ai);
+    i32 bp, ap, bq, aq, bdist = 0, adist = 0, bpost = 0, apost = 0;
+    if (kind == HFTLOB_MM_ACT_BOB_RL || kind == HFTLOB_MM_ACT_BOB_STRATEGY || kind == HFTLOB_MM_ACT_AVST) {
+        i32 ba, bb;
+        const bool empty = masked_best(c, B, tid, last_ba, last_bb, ba, bb);
+        if (kind == HFTLOB_MM_ACT_BOB_RL) {  // :1474-1561; tables bid v0 + (+k, -k, ...) / ask v0 - ...
+            const i32 v0 = tc.bob_v0, d = (ai & 1) ? (ai + 1) / 2 : -(ai / 2);
+            bq = wmul(wadd(v0, d), fq);
+            aq = wmul(wsub(v0, d), fq);
+            if (empty) { bq = 0; aq = 0; }
+            bp = bb; ap = ba;
+        } else if (kind == HFTLOB_MM_ACT_BOB_STRATEGY) {  // :1400-1472
+            const float kappa = i2f(wadd(action, 1)) / i2f(wmul(tc.bob_v0, 5));
+            const float pos = i2f(inv), v0 = (float)tc.bob_v0;
+            bq = f2i_sat(rintf(v0 * fmaxf(1.0f - kappa * pos, 0.0f)));
+            aq = f2i_sat(rintf(v0 * fmaxf(1.0f + kappa * pos, 0.0f)));
+            if (empty) { bq = 0; aq = 0; }
+            bp = bb; ap = ba;
+        } else {  // AvSt :1248-1398
+            const i32 mid = ifloordiv(wadd(ba, bb), 2);
+            const float gam[8] = {0.1f, 0.2f, 0.5f, 1.0f, 2.0f, 5.0f, 10.0f, 20.0f};
+            float gamma = gam[0], lt = tc.avst_log_term[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) if (ai == k) { gamma = gam[k]; lt = tc.avst_log_term[k]; }
+            const i32 tl = c.ep_type == 1 ? wsub(c.episode_time, wsub(wt0, init_t0)) : wsub(c.episode_time, step);
+            const float nt = i2f(tl) / i2f(c.episode_time);
+            const float res = i2f(mid) - i2f(inv) * gamma * tc.avst_var * nt;
+            float spread = gamma * tc.avst_var * nt + (2.0f / gamma) * lt;
+            spread = fminf(fmaxf(spread, (float)tick), (float)c.lob.maxint);
+            float bf = res - spread / 2.0f, af = res + spread / 2.0f;
+            bf = fminf(fmaxf(bf, 0.0f), (float)c.lob.maxint);
+            af = fminf(fmaxf(af, 0.0f), (float)c.lob.maxint);
+            bp = f2i_sat(ffloordiv(bf, (float)tick) * (float)tick);
+            ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
+            const i32 q = ifloordiv(mid, tick), rm = wsub(mid, wmul(q, tick));
+            bp = imin_(bp, wmul(wsub(q, rm == 0 ? 1 : 0), tick));  // round_down: strictly below mid
+            ap = imax_(ap, wmul(wadd(q, 1), tick));                // round_up: strictly above mid
+            bq = fq; aq = fq;
+            bdist = wsub(bb, bp); adist = wsub(ap, ba); bpost = bp; apost = ap;
+        }
+    } else {
+        const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
+        if (kind == HFTLOB_MM_ACT_SPREAD_SKEW) {  // :1667-1808
+            const float mid = i2f(wadd(ba, bb)) / 2.0f;
+            const i32 cur = wsub(ba, bb);
+            const i32 st_ = ifloordiv(action, 3), sk = wsub(action, wmul(st_, 3));
+            const float mult = st_ == 0 ? 1.0f : tc.spread_multiplier;
+            const float nsp = i2f(cur) * mult;
+            const float skt = sk == 0 ? -tc.skew_multiplier : (sk == 1 ? 0.0f : tc.skew_multiplier);
+            const float smid = mid + skt * (tc.multiplier_type ? nsp : (float)tick);
+            const float hs = ffloordiv(nsp, 2.0f);
+            bp = f2i_sat(ffloordiv(smid - hs, (float)tick) * (float)tick);
+            ap = f2i_sat(ffloordiv(smid + hs, (float)tick) * (float)tick);
+            bq = fq; aq = fq;
+        } else {  // simple :1123-1246
+            const float bo = ai == 1 ? -2000.0f : 0.0f, ao = ai == 2 ? -2000.0f : 0.0f;
+            if (tc.sell_buy_all_option) {
+                const i32 big = imax_(iabs_(inv), fq);
+                const i32 bqa = inv > 0 ? fq : big, aqa = inv > 0 ? big : fq;
+                bq = ai == 0 ? fq : (ai == 1 ? bqa : 0);
+                aq = ai == 0 ? fq : (ai == 2 ? aqa : 0);
+            } else {
+                bq = wmul((ai == 0 || ai == 1) ? 1 : 0, fq);
+                aq = wmul((ai == 0 || ai == 2) ? 1 : 0, fq);
+            }
+            // entry 3 (simple_nothing_action) is all zeros; with 3 entries `ai` clamps to 2
+            const float to = (float)wmul(tc.n_ticks_offset, tick);
+            const float bf = i2f(bb) - bo * to, af = i2f(ba) + ao * to;
+            bp = f2i_sat(ffloordiv(fmaxf(bf, 0.0f), (float)tick) * (float)tick);
+            ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
+        }
+    }
+    const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
+    put_row(lds_rows, row, 1, 1, bq, bp, c.placeholder_order_id, tid, ta, tb);
+    put_row(lds_rows, row + 1, 1, -1, aq, ap, c.placeholder_order_id, tid, ta, tb);
+    x.bid_price = bpost; x.ask_price = apost; x.bid_dist = bdist; x.ask_dist = adist;
     x.bid_quant = bq; x.ask_quant = aq;
 }
 
@@ -1582,12 +1687,16 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     const i32 pen = wmul(tc.doom_price_penalty, tick);
     const i32 side_sign = wsub(wmul(sell, 2), 1);
     i32 refp;
-    if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)
+    const float penf = tc.doom_penalty_is_float ? tc.doom_penalty_f32 : i2f(pen);
+    if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH && !tc.doom_penalty_is_float)
         refp = sell ? wmul(ifloordiv(wsub(X.last_bb, pen), tick), tick)
                     : wmul(ifloordiv(wadd(X.last_ba, pen), tick), tick);
+    else if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)  // int32 price - Python float: f32
+        refp = sell ? f2i(ffloordiv(i2f(X.last_bb) - penf, (float)tick) * (float)tick)
+                    : f2i(ffloordiv(i2f(X.last_ba) + penf, (float)tick) * (float)tick);
     else
-        refp = sell ? f2i(ffloordiv(X.avg_mid - i2f(pen), (float)tick) * (float)tick)
-                    : f2i(ffloordiv(X.avg_mid + i2f(pen), (float)tick) * (float)tick);
+        refp = sell ? f2i(ffloordiv(X.avg_mid - penf, (float)tick) * (float)tick)
+                    : f2i(ffloordiv(X.avg_mid + penf, (float)tick) * (float)tick);
     const bool add = X.ep_done && quant_left > 0;
     const i32 ovr[8] = {refp, wmul(side_sign, iabs_(quant_left)), c.artificial_order_id, c.placeholder_order_id,
                         0, 0, c.artificial_trader_id, tid};
@@ -1820,8 +1929,11 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                 if (tc.kind == HFTLOB_AGENT_MM) {
                     if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
                         mm_directional(c, tc, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
-                    else
+                    else if (tc.action_space == HFTLOB_MM_ACT_FIXED_QUANTS)
                         mm_fixed_quant(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
+                    else
+                        mm_other_actions(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, ld_t0, rows,
+                                         arow, x);
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
                     const int sz = tc.n_msgs / 4;
@@ -2171,7 +2283,12 @@ static int check_env(const hftlob_env_cfg* c) {
         const hftlob_agent_type_cfg& tc = c->types[t];
         agents += tc.n_agents;
         if (tc.kind == HFTLOB_AGENT_MM) {
-            if (tc.sell_buy_all_option) return fail(HFTLOB_EINVAL, "MM sell_buy_all_option unsupported");
+            if (tc.sell_buy_all_option && tc.action_space != HFTLOB_MM_ACT_SIMPLE)
+                return fail(HFTLOB_EINVAL, "MM sell_buy_all_option: simple action space only");
+            if (tc.action_space < 0 || tc.action_space > HFTLOB_MM_ACT_SIMPLE) return fail(HFTLOB_EINVAL, "MM action_space");
+            if ((tc.action_space == HFTLOB_MM_ACT_BOB_RL || tc.action_space == HFTLOB_MM_ACT_BOB_STRATEGY) &&
+                tc.bob_v0 <= 0)
+                return fail(HFTLOB_EINVAL, "bob_v0 must be positive");
             if (tc.n_action_msgs != 2 || tc.n_msgs != 4) return fail(HFTLOB_EINVAL, "MM message counts");
         } else if (tc.kind == HFTLOB_AGENT_EXE) {
             if (tc.n_action_msgs != 4 || tc.n_msgs != 8) return fail(HFTLOB_EINVAL, "EXE message counts");

@@ -10,8 +10,11 @@ accesses; named torch views over it reproduce the reference state pytrees
 from __future__ import annotations
 
 import ctypes as C
+import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Tuple
+
+import numpy as np
 
 from .config import (Execution_EnvironmentConfig, MarketMaking_EnvironmentConfig,
                      MultiAgentConfig)
@@ -47,7 +50,11 @@ class AgentTypeCfg(C.Structure):
         "rebate_bps", "unrealizedPnL_lambda")] + [
         ("task", C.c_int32), ("task_size", C.c_int32), ("n_ticks_in_book", C.c_int32),
         ("doom_price_penalty", C.c_int32), ("reward_lambda", C.c_float),
-        ("rebate_factor", C.c_float), ("one_minus_eta", C.c_float), ("_pad", C.c_int32)]
+        ("rebate_factor", C.c_float), ("one_minus_eta", C.c_float),
+        ("bob_v0", C.c_int32), ("n_ticks_offset", C.c_int32), ("simple_nothing_action", C.c_int32),
+        ("multiplier_type", C.c_int32), ("spread_multiplier", C.c_float), ("skew_multiplier", C.c_float),
+        ("avst_var", C.c_float), ("avst_k", C.c_float), ("avst_log_term", C.c_float * 8),
+        ("doom_penalty_is_float", C.c_int32), ("doom_penalty_f32", C.c_float)]
 
 
 class EnvCfg(C.Structure):
@@ -67,7 +74,9 @@ class StepOut(C.Structure):
 
 
 # ----------------------------------------------------------- enum mappings
-MM_ACTION = {"fixed_quants": 0, "directional_trading": 1}
+MM_ACTION = {"fixed_quants": 0, "directional_trading": 1, "bobRL": 2, "bobStrategy": 3, "AvSt": 4,
+             "spread_skew": 5, "simple": 6}
+AVST_GAMMA = (0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 20.0)       # mm_env.py:1283
 MM_OBS = {"basic": 0, "engineered": 1}
 MM_REWARD = {"portfolio_value": 0, "buy_sell_pnl": 1, "complex": 2, "zero_inv": 3, "spooner": 4,
              "spooner_damped": 5, "spooner_asym_damped": 6, "spooner_asym_damped2": 7,
@@ -195,16 +204,21 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
     a.reward_scaling_quo = _f(t.reward_scaling_quo)
     if isinstance(t, MarketMaking_EnvironmentConfig):
         a.kind = AGENT_MM
+        if t.action_space == "fixed_prices":
+            raise NotImplementedError("MM action_space 'fixed_prices': the reference's _getActionMsgs_fixedPrice "
+                                      "reads an undefined `state` (mm_env.py:1625, NameError at trace time)")
         if t.action_space not in MM_ACTION:
-            raise NotImplementedError(f"MM action_space {t.action_space!r} not implemented on the HIP path")
+            raise ValueError("Invalid action_space specified.")
         if t.observation_space not in MM_OBS:
             raise NotImplementedError(f"MM observation_space {t.observation_space!r} not implemented")
         if t.reward_function not in MM_REWARD:
             raise ValueError("Invalid reward_space specified.")
         if t.inv_penalty not in INV_PEN:
             raise NotImplementedError(f"inv_penalty {t.inv_penalty!r} not implemented")
-        if t.sell_buy_all_option:
-            raise NotImplementedError("sell_buy_all_option=True not implemented")
+        if t.sell_buy_all_option and t.action_space not in ("simple",):
+            raise NotImplementedError("sell_buy_all_option=True is implemented for the 'simple' action space")
+        if t.action_space == "spread_skew" and t.multiplier_type not in ("tick", "spread"):
+            raise ValueError(f"multiplier_type {t.multiplier_type!r}")
         if t.unwind_price not in ("mid", "mid_avg", "far_touch"):
             raise ValueError("Invalid unwind price type.")
         a.action_space, a.observation_space = MM_ACTION[t.action_space], MM_OBS[t.observation_space]
@@ -224,6 +238,14 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
         a.rebate_bps, a.unrealizedPnL_lambda = _f(t.rebate_bps), _f(t.unrealizedPnL_lambda)
         a.rebate_factor = _f(t.rebate_bps / 10_000)          # formed in Python double (mm_env.py:2369)
         a.one_minus_eta = _f(1 - t.inventoryPnL_eta)          # mm_env.py:2434
+        a.bob_v0, a.n_ticks_offset = t.bob_v0, t.n_ticks_offset
+        a.simple_nothing_action = int(t.simple_nothing_action)
+        a.multiplier_type = int(t.multiplier_type == "spread")
+        a.spread_multiplier, a.skew_multiplier = _f(t.spread_multiplier), _f(t.skew_multiplier)
+        a.avst_var, a.avst_k = _f(t.avst_var_parameter), _f(t.avst_k_parameter)
+        for i, g in enumerate(AVST_GAMMA):                    # f32 gamma / f32 k, + 1 in f32, log rounded once
+            q = np.float32(np.float32(g) / np.float32(t.avst_k_parameter))
+            a.avst_log_term[i] = float(np.float32(math.log(float(np.float32(np.float32(1.0) + q)))))
     else:
         a.kind = AGENT_EXE
         if t.action_space not in EXE_ACTION:
@@ -239,7 +261,13 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
         if t.task not in TASK:
             raise ValueError(f"invalid task {t.task!r}")
         a.task, a.task_size, a.n_ticks_in_book = TASK[t.task], t.task_size, t.n_ticks_in_book
-        a.doom_price_penalty, a.reward_lambda = t.doom_price_penalty, _f(t.reward_lambda)
+        a.reward_lambda = _f(t.reward_lambda)
+        pen = t.doom_price_penalty
+        if isinstance(pen, float) and not pen.is_integer():
+            a.doom_penalty_is_float, a.doom_penalty_f32 = 1, _f(pen * world.tick_size)
+        else:
+            a.doom_price_penalty = int(pen)
+            a.doom_penalty_f32 = _f(int(pen) * world.tick_size)
     return a
 
 

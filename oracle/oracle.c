@@ -563,6 +563,129 @@ static void mm_fixed_quant(const hftlob_env_cfg* c, const hftlob_agent_type_cfg*
     x->bid_quant = bquant; x->ask_quant = aquant; x->empty_book = empty;
 }
 
+/* XLA f32 -> s32 convert (saturating; NaN -> 0) */
+static i32 f2i_sat(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (i32)f;
+}
+/* jnp table[idx] on a traced index: negative indices wrap once, then clamp */
+static int gather_idx(i32 a, int n) {
+    i32 i = a < 0 ? a + n : a;
+    return i < 0 ? 0 : (i >= n ? n - 1 : i);
+}
+
+/* MM bobRL (:1474-1561), bobStrategy (:1400-1472), AvSt (:1248-1398),
+ * spread_skew (:1667-1808), simple (:1123-1246) */
+static void mm_other_actions(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env* E, const i32* st, i32 tid,
+                             i32 action, i32* out, ActX* x) {
+    static const i32 bob1b[3] = {1, 2, 0}, bob1a[3] = {1, 0, 2};
+    static const i32 bob2b[5] = {2, 3, 1, 4, 0}, bob2a[5] = {2, 1, 3, 0, 4};
+    static const i32 bob5b[11] = {5, 6, 4, 7, 3, 8, 2, 9, 1, 10, 0}, bob5a[11] = {5, 4, 6, 3, 7, 2, 8, 1, 9, 0, 10};
+    static const i32 bob10b[21] = {10, 11, 9, 12, 8, 13, 7, 14, 6, 15, 5, 16, 4, 17, 3, 18, 2, 19, 1, 20, 0};
+    static const i32 bob10a[21] = {10, 9, 11, 8, 12, 7, 13, 6, 14, 5, 15, 4, 16, 3, 17, 2, 18, 1, 19, 0, 20};
+    static const float gammas[8] = {0.1f, 0.2f, 0.5f, 1.0f, 2.0f, 5.0f, 10.0f, 20.0f};
+    if (tc->fixed_action_setting) action = tc->fixed_action;
+    i32 tick = c->tick_size, inv = st[2], fq = tc->fixed_quant_value;
+    i32 lba = BASKS(E)[(c->n_msgs - 1) * 2], lbb = BBIDS(E)[(c->n_msgs - 1) * 2];
+    i32 bp = 0, ap = 0, bq = 0, aq = 0;
+    x->bid_price = x->ask_price = x->bid_dist = x->ask_dist = 0;
+    x->empty_book = 0;
+    int kind = tc->action_space;
+    if (kind == HFTLOB_MM_ACT_BOB_RL || kind == HFTLOB_MM_ACT_BOB_STRATEGY || kind == HFTLOB_MM_ACT_AVST) {
+        i32 ba, bb;
+        masked_best(c, ASKS(E), BIDS(E), tid, &ba, &bb);
+        int empty = (ba == -1) || (bb == -1);
+        ba = wmul(ifloordiv(ba, tick), tick);
+        bb = wmul(ifloordiv(bb, tick), tick);
+        if (empty) { bb = lbb; ba = lba; }
+        if (kind == HFTLOB_MM_ACT_BOB_RL) {
+            const i32 *tb, *ta;
+            int n;
+            switch (tc->bob_v0) {
+                case 1: tb = bob1b; ta = bob1a; n = 3; break;
+                case 2: tb = bob2b; ta = bob2a; n = 5; break;
+                case 5: tb = bob5b; ta = bob5a; n = 11; break;
+                default: tb = bob10b; ta = bob10a; n = 21; break;
+            }
+            int i = gather_idx(action, n);
+            bq = empty ? 0 : wmul(tb[i], fq);
+            aq = empty ? 0 : wmul(ta[i], fq);
+            bp = bb; ap = ba;
+        } else if (kind == HFTLOB_MM_ACT_BOB_STRATEGY) {
+            float kappa = i2f(wadd(action, 1)) / i2f(wmul(tc->bob_v0, 5));
+            float v0 = (float)tc->bob_v0;
+            bq = f2i_sat(rintf(v0 * fmaxf(1.0f - kappa * i2f(inv), 0.0f)));
+            aq = f2i_sat(rintf(v0 * fmaxf(1.0f + kappa * i2f(inv), 0.0f)));
+            if (empty) bq = aq = 0;
+            bp = bb; ap = ba;
+        } else {
+            i32 mid = ifloordiv(wadd(ba, bb), 2);
+            int i = gather_idx(action, 8);
+            float gamma = gammas[i];
+            const i32* L = LOADED(E);
+            i32 tl = c->ep_type == 1 ? wsub(c->episode_time, wsub(WORLD(E)[0], L[0])) : wsub(c->episode_time, L[5]);
+            float nt = i2f(tl) / i2f(c->episode_time);
+            float res = i2f(mid) - i2f(inv) * gamma * tc->avst_var * nt;
+            float spread = gamma * tc->avst_var * nt + (2.0f / gamma) * tc->avst_log_term[i];
+            spread = fminf(fmaxf(spread, (float)tick), (float)c->lob.maxint);
+            float bf = fminf(fmaxf(res - spread / 2.0f, 0.0f), (float)c->lob.maxint);
+            float af = fminf(fmaxf(res + spread / 2.0f, 0.0f), (float)c->lob.maxint);
+            bp = f2i_sat(ffloordiv(bf, (float)tick) * (float)tick);
+            ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
+            i32 q = ifloordiv(mid, tick), m = wsub(mid, wmul(q, tick));
+            i32 rdown = wmul(wsub(q, m == 0 ? 1 : 0), tick), rup = wmul(wadd(q, 1), tick);
+            bp = imin(bp, rdown);
+            ap = imax(ap, rup);
+            bq = aq = fq;
+            x->bid_price = bp; x->ask_price = ap; x->bid_dist = wsub(bb, bp); x->ask_dist = wsub(ap, ba);
+        }
+        if (kind != HFTLOB_MM_ACT_AVST) x->empty_book = empty;
+    } else {
+        i32 ba = wmul(ifloordiv(lba, tick), tick), bb = wmul(ifloordiv(lbb, tick), tick);
+        if (kind == HFTLOB_MM_ACT_SPREAD_SKEW) {
+            float mid = i2f(wadd(ba, bb)) / 2.0f;
+            i32 cur = wsub(ba, bb);
+            i32 stype = ifloordiv(action, 3), skew = wsub(action, wmul(stype, 3));
+            float mult = stype == 0 ? 1.0f : tc->spread_multiplier;
+            float nsp = i2f(cur) * mult;
+            float skt = skew == 0 ? -tc->skew_multiplier : (skew == 1 ? 0.0f : tc->skew_multiplier);
+            float smid = tc->multiplier_type ? mid + skt * nsp : mid + skt * (float)tick;
+            float hs = ffloordiv(nsp, 2.0f);
+            bp = f2i_sat(ffloordiv(smid - hs, (float)tick) * (float)tick);
+            ap = f2i_sat(ffloordiv(smid + hs, (float)tick) * (float)tick);
+            bq = aq = fq;
+        } else {
+            static const float boffs[4] = {0, -2000, 0, 0}, aoffs[4] = {0, 0, -2000, 0};
+            int n = tc->simple_nothing_action ? 4 : 3;
+            int i = gather_idx(action, n);
+            if (tc->sell_buy_all_option) {
+                i32 bqa, aqa;
+                if (inv > 0) { bqa = fq; aqa = imax(iabs(inv), fq); }
+                else { bqa = imax(iabs(inv), fq); aqa = fq; }
+                i32 tbq[4] = {fq, bqa, 0, 0}, taq[4] = {fq, 0, aqa, 0};
+                bq = tbq[i]; aq = taq[i];
+            } else {
+                static const i32 tbq[4] = {1, 1, 0, 0}, taq[4] = {1, 0, 1, 0};
+                bq = wmul(tbq[i], fq); aq = wmul(taq[i], fq);
+            }
+            float to = (float)wmul(tc->n_ticks_offset, tick);
+            float bf = i2f(bb) - boffs[i] * to, af = i2f(ba) + aoffs[i] * to;
+            bp = f2i_sat(ffloordiv(fmaxf(bf, 0.0f), (float)tick) * (float)tick);
+            ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
+        }
+    }
+    i32 q[2] = {bq, aq}, p[2] = {bp, ap}, sd[2] = {1, -1};
+    const i32* wt = WORLD(E);
+    for (int k = 0; k < 2; ++k) {
+        i32* o = out + k * 8;
+        o[0] = 1; o[1] = sd[k]; o[2] = q[k]; o[3] = p[k]; o[4] = c->placeholder_order_id; o[5] = tid;
+        o[6] = wadd(wt[0], tc->time_delay_obs_act); o[7] = wadd(wt[1], tc->time_delay_obs_act);
+    }
+    x->bid_quant = bq; x->ask_quant = aq;
+}
+
 /* MM _getActionMsgs_directional_trading — mm_env.py:1810-1865 */
 static void mm_directional(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env* E, i32 tid, i32 action,
                            i32* out, ActX* x) {
@@ -839,12 +962,17 @@ static void exe_reward(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc,
     float avg_mid = wsum(mids, M) / (float)M;
     i32 side_sign = wsub(wmul(sell, 2), 1);
     i32 refp;
-    if (tc->reference_price == HFTLOB_PRICE_FAR_TOUCH)
+    /* a non-integer doom_price_penalty is a Python float: the far-touch price is then f32 */
+    float penf = tc->doom_penalty_is_float ? tc->doom_penalty_f32 : i2f(pen);
+    if (tc->reference_price == HFTLOB_PRICE_FAR_TOUCH && !tc->doom_penalty_is_float)
         refp = sell ? wmul(ifloordiv(wsub(bbb[(M - 1) * 2], pen), tick), tick)
                     : wmul(ifloordiv(wadd(bba[(M - 1) * 2], pen), tick), tick);
+    else if (tc->reference_price == HFTLOB_PRICE_FAR_TOUCH)
+        refp = sell ? f2i(ffloordiv(i2f(bbb[(M - 1) * 2]) - penf, (float)tick) * (float)tick)
+                    : f2i(ffloordiv(i2f(bba[(M - 1) * 2]) + penf, (float)tick) * (float)tick);
     else
-        refp = sell ? f2i(ffloordiv(avg_mid - i2f(pen), (float)tick) * (float)tick)
-                    : f2i(ffloordiv(avg_mid + i2f(pen), (float)tick) * (float)tick);
+        refp = sell ? f2i(ffloordiv(avg_mid - penf, (float)tick) * (float)tick)
+                    : f2i(ffloordiv(avg_mid + penf, (float)tick) * (float)tick);
     if (ep_done && quant_left > 0) {
         i32 row[8] = {refp, wmul(side_sign, iabs(quant_left)), c->artificial_order_id, c->placeholder_order_id,
                       0, 0, c->artificial_trader_id, tid};
@@ -1051,7 +1179,7 @@ static int env_cfg_ok(const hftlob_env_cfg* c) {
     if (c->obs_stride > HFTLOB_MAX_OBS) return 0;
     for (int t = 0; t < c->n_types; ++t) {
         const hftlob_agent_type_cfg* tc = &c->types[t];
-        if (tc->kind == HFTLOB_AGENT_MM && tc->sell_buy_all_option) return 0;
+        if (tc->kind == HFTLOB_AGENT_MM && tc->sell_buy_all_option && tc->action_space != HFTLOB_MM_ACT_SIMPLE) return 0;
     }
     return 1;
 }
@@ -1107,7 +1235,8 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
             memset(&ax[a], 0, sizeof ax[a]);
             if (tc->kind == HFTLOB_AGENT_MM) {
                 if (tc->action_space == HFTLOB_MM_ACT_DIRECTIONAL) mm_directional(c, tc, &E, tid, act[a], am, &ax[a]);
-                else mm_fixed_quant(c, tc, &E, st, tid, act[a], am, &ax[a]);
+                else if (tc->action_space == HFTLOB_MM_ACT_FIXED_QUANTS) mm_fixed_quant(c, tc, &E, st, tid, act[a], am, &ax[a]);
+                else mm_other_actions(c, tc, &E, st, tid, act[a], am, &ax[a]);
                 int sz = tc->n_msgs / 4;
                 get_cancel_msgs(BIDS(&E), nO, tid, sz, 1, W[0], W[1], cm);
                 get_cancel_msgs(ASKS(&E), nO, tid, sz, -1, W[0], W[1], cm + sz * 8);
@@ -1285,6 +1414,33 @@ void oracle_sample_actions(const hftlob_env_cfg* c, int n_env, const u32* keys, 
 void oracle_split_keys(int n_env, int n, int part, const u32* keys, u32* out) {
     for (int e = 0; e < n_env; ++e)
         for (int j = 0; j < n; ++j) oracle_split(keys + 2 * e, n, j, part, out + ((size_t)e * n + j) * 2);
+}
+
+/* One MM agent's raw action messages (before _filter_messages) for the env
+ * record `rec`: the agent-level checker of the action spaces (tests only).
+ * out: 2 rows of 8; extras: bid_price, ask_price, bid_dist, ask_dist, bid_quant,
+ * ask_quant, empty_book. */
+int oracle_mm_action_msgs(const hftlob_env_cfg* c, int type, int agent, const i32* rec, i32 action, i32* out,
+                          i32* extras) {
+    if (type < 0 || type >= c->n_types || c->types[type].kind != HFTLOB_AGENT_MM) return HFTLOB_EINVAL;
+    const hftlob_agent_type_cfg* tc = &c->types[type];
+    Env E = {c, (i32*)rec};
+    int a0 = 0, off = c->off_agents;
+    for (int t = 0; t < type; ++t) {
+        a0 += c->types[t].n_agents;
+        off += c->types[t].n_agents * agent_words(&c->types[t]);
+    }
+    const i32* st = rec + off + agent * agent_words(tc);
+    i32 tid = wsub(tc->trader_id0, agent);
+    ActX x;
+    memset(&x, 0, sizeof x);
+    if (tc->action_space == HFTLOB_MM_ACT_DIRECTIONAL) mm_directional(c, tc, &E, tid, action, out, &x);
+    else if (tc->action_space == HFTLOB_MM_ACT_FIXED_QUANTS) mm_fixed_quant(c, tc, &E, st, tid, action, out, &x);
+    else mm_other_actions(c, tc, &E, st, tid, action, out, &x);
+    i32 ex[7] = {x.bid_price, x.ask_price, x.bid_dist, x.ask_dist, x.bid_quant, x.ask_quant, x.empty_book};
+    memcpy(extras, ex, sizeof ex);
+    (void)a0;
+    return HFTLOB_OK;
 }
 
 /* struct layout of include/hftlob.h as the C compiler sees it (ABI test) */

@@ -33,6 +33,7 @@ def lib():
         L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
         L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
+        L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int32, vp, vp]
         L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
         L.oracle_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)] * 2
         L.oracle_randint.argtypes = [vp, C.c_int32, C.c_int32, C.c_int]
@@ -118,6 +119,15 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
                                _p(np.ascontiguousarray(init_states, np.int32)), _p(st), _p(obs), _p(rew), _p(da),
                                _p(dn), _p(info)))
     return st, obs, rew, da, dn, info
+
+
+def mm_action_msgs(env_cfg, type_idx, agent, rec, action):
+    """(rows int32 [2, 8], extras [7]) of one MM agent's raw action messages for record `rec`."""
+    out = np.zeros((2, 8), np.int32)
+    ex = np.zeros(7, np.int32)
+    rec = np.ascontiguousarray(rec, dtype=np.int32)
+    _chk(lib().oracle_mm_action_msgs(C.byref(env_cfg), type_idx, agent, _p(rec), int(action), _p(out), _p(ex)))
+    return out, ex
 
 
 def sample_actions(env_cfg, keys):

@@ -183,8 +183,39 @@ def test_mm_option_parity(changes):
     rollout_parity(variant(builtin_config("2_player_fq_fqc"), "MarketMaking", **changes), E=32, K=66)
 
 
+MM_ACTION_VARIANTS = [
+    dict(action_space="bobRL", bob_v0=1), dict(action_space="bobRL", bob_v0=2, fixed_quant_value=3),
+    dict(action_space="bobRL", bob_v0=5), dict(action_space="bobRL", bob_v0=10),
+    dict(action_space="bobStrategy", bob_v0=2), dict(action_space="bobStrategy", bob_v0=5, fixed_quant_value=1),
+    dict(action_space="AvSt"), dict(action_space="AvSt", avst_k_parameter=1.5, avst_var_parameter=2000.0),
+    dict(action_space="spread_skew"),
+    dict(action_space="spread_skew", multiplier_type="spread", spread_multiplier=2.0, skew_multiplier=0.5),
+    dict(action_space="simple"), dict(action_space="simple", simple_nothing_action=False, n_ticks_offset=2),
+    dict(action_space="simple", sell_buy_all_option=True, fixed_quant_value=2),
+    dict(action_space="bobRL", bob_v0=2, fixed_action_setting=True, fixed_action=3),
+]
+
+
+@pytest.mark.parametrize("changes", MM_ACTION_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+def test_mm_action_space_parity(changes):
+    """MM action spaces bobRL / bobStrategy / AvSt / spread_skew / simple (mm_env.py:1123-1809)."""
+    rollout_parity(variant(builtin_config("2_player_fq_fqc"), "MarketMaking", **changes), E=32, K=66)
+
+
+def test_mm_avst_fixed_time(tmp_path_factory):
+    """AvSt's time_left under fixed_time episodes (mm_env.py:1287-1290) on loader-built windows."""
+    day = _loaded("fixed_time", str(tmp_path_factory.mktemp("lob")))
+    cfg = builtin_config("2_player_fq_fqc")
+    w = dataclasses.replace(cfg.world_config, ep_type="fixed_time", episode_time=300, start_resolution=300)
+    cfg = variant(dataclasses.replace(cfg, world_config=w), "MarketMaking", action_space="AvSt",
+                  avst_var_parameter=500.0)
+    rollout_parity(cfg, E=32, K=20, day=day)
+
+
 EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid", task="buy"),
-                dict(task="sell", normalize=False)]
+                dict(task="sell", normalize=False),
+                dict(doom_price_penalty=0.1),                    # Python-float penalty: f32 far-touch price
+                dict(doom_price_penalty=0.37, reference_price="mid")]
 
 
 @pytest.mark.parametrize("changes", EXE_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
