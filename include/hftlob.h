@@ -77,8 +77,9 @@ enum { HFTLOB_PRICE_MID = 0, HFTLOB_PRICE_MID_AVG = 1, HFTLOB_PRICE_FAR_TOUCH = 
        HFTLOB_PRICE_NEAR_TOUCH = 3 };
 enum { HFTLOB_INVPEN_NONE = 0, HFTLOB_INVPEN_LINEAR, HFTLOB_INVPEN_QUADRATIC,
        HFTLOB_INVPEN_THRESHOLD };
-enum { HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX = 0 };
-enum { HFTLOB_EXE_OBS_ENGINEERED = 0 };
+enum { HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX = 0, HFTLOB_EXE_ACT_SIMPLEST_CASE = 1, HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG = 2,
+       HFTLOB_EXE_ACT_TWAP = 3 };
+enum { HFTLOB_EXE_OBS_ENGINEERED = 0, HFTLOB_EXE_OBS_BASIC = 1, HFTLOB_EXE_OBS_SIMPLEST_CASE = 2 };
 enum { HFTLOB_EXE_REW_NORMAL = 0, HFTLOB_EXE_REW_FINISH_FAST = 1 };
 enum { HFTLOB_TASK_RANDOM = 0, HFTLOB_TASK_BUY = 1, HFTLOB_TASK_SELL = 2 };
 

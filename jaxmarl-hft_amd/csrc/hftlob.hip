@@ -1019,6 +1019,23 @@ DEV void mm_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* 
 DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o,
                  bool ftime) {
     const bool nz = tc.normalize;
+    if (tc.observation_space == HFTLOB_EXE_OBS_BASIC) {  // :1879-1911 best_ask_price, best_bid_price, remaining_quant
+        const i32 rq = wsub(st[1], st[2]);
+        o[0] = nz ? i2f(wsub(w.best_ask_p, 1550000)) / 1e3f : i2f(w.best_ask_p);
+        o[1] = nz ? i2f(wsub(w.best_bid_p, 1550000)) / 1e3f : i2f(w.best_bid_p);
+        o[2] = nz ? i2f(rq) / (float)tc.task_size : i2f(rq);
+        return;
+    }
+    if (tc.observation_space == HFTLOB_EXE_OBS_SIMPLEST_CASE) {
+        // :1841-1877 mid_price, percent_remaining_quant, percent_time_remaining
+        const float ep = (float)c.episode_time;
+        const float ptr = (ep - (i2f(wsub(w.t0, w.it0)) + i2f(wsub(w.t1, w.it1)) / 1e9f)) / ep;
+        const float prq = i2f(wsub(st[1], st[2])) / i2f(st[1]);
+        o[0] = nz ? (w.mid - 7560000.0f) / 1e3f : w.mid;
+        o[1] = nz ? (prq - 0.5f) / 1.0f : prq;
+        o[2] = nz ? (ptr - 0.5f) / 1.0f : ptr;
+        return;
+    }
     const i32 sell = st[3];
     const i32 p_aggr = sell ? w.best_bid_p : w.best_ask_p, p_pass = sell ? w.best_ask_p : w.best_bid_p;
     const i32 q_aggr = sell ? w.vol_b : w.vol_a, q_pass = sell ? w.vol_a : w.vol_b;
@@ -1292,7 +1309,7 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
     const bool empty = masked_best(c, B, tid, last_ba, last_bb, ba, bb);
     const float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
     const float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
-    const int ai = action < 0 ? 0 : (action > 9 ? 9 : action);
+    const int ai = action < 0 ? imax_(action + 10, 0) : (action > 9 ? 9 : action);  // jnp gather index
     // offsets tables {0,1,2,3,4,0,2,5,1,0} / {0,1,2,3,4,2,0,1,5,0}; quants 1.. ,0
     const float bo = (float)((0x0152043210ull >> (4 * ai)) & 0xF);
     const float ao = (float)((0x0510243210ull >> (4 * ai)) & 0xF);
@@ -1418,7 +1435,7 @@ DEV void mm_directional(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
                         i32 last_ba, i32 last_bb, i32* lds_rows, int row, ActX& x) {
     const i32 tick = c.tick_size;
     const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
-    const int ai = action < 0 ? 0 : (action > 2 ? 2 : action);
+    const int ai = action < 0 ? imax_(action + 3, 0) : (action > 2 ? 2 : action);
     const i32 bq = (ai == 1) * tc.fixed_quant_value, aq = (ai == 2) * tc.fixed_quant_value;
     const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
     put_row(lds_rows, row, 1, 1, bq, ba, c.placeholder_order_id, tid, ta, tb);
@@ -1428,8 +1445,9 @@ DEV void mm_directional(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
 }
 
 // EXE _getActionMsgs_fixedQuant_extended — exec_env.py:838-932
+// + simplest_case (:935-999), fixed_quants_1msg (:732-836), twap (:1126-1227): rows = n_action_msgs
 DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const i32* st, i32 tid, i32 action, i32 wt0,
-                 i32 wt1, i32 last_ba, i32 last_bb, i32* lds_rows, int row) {
+                 i32 wt1, i32 last_ba, i32 last_bb, i32 step, i32 max_steps, i32* lds_rows, int row) {
     const i32 tick = c.tick_size;
     const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
     const i32 sell = st[3];
@@ -1445,19 +1463,46 @@ DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
         pl[2] = bb;
         pl[3] = wsub(bb, wmul(tick, tc.n_ticks_in_book));
     }
-    const int ai = action < 0 ? 0 : (action > 12 ? 12 : action);
-    // quant table rows: action 0 -> none; 1..12 -> level (ai-1)%4 with multiple {1,2,5}[(ai-1)/4]
-    i32 q[4] = {0, 0, 0, 0};
-    if (ai > 0) {
-        const int lvl = (ai - 1) & 3, mul = (ai - 1) >> 2;
-        q[lvl] = wmul(mul == 0 ? 1 : (mul == 1 ? 2 : 5), tc.fixed_quant_value);
-    }
-    const i32 tot = wadd(wadd(q[0], q[1]), wadd(q[2], q[3]));
-    const i32 left = wsub(st[1], st[2]);
-    if (!(tot <= left)) { q[0] = f2i(floorf(i2f(left))); q[1] = q[2] = q[3] = 0; }
     const i32 side = wsub(1, wmul(sell, 2));
     const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
-    for (int k = 0; k < 4; ++k) put_row(lds_rows, row + k, 1, side, q[k], pl[k], c.placeholder_order_id, tid, ta, tb);
+    const i32 fq = tc.fixed_quant_value, left = wsub(st[1], st[2]);
+    i32 q[4] = {0, 0, 0, 0};
+    if (tc.action_space == HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX) {
+        const int ai = action < 0 ? imax_(action + 13, 0) : (action > 12 ? 12 : action);
+        // quant table rows: action 0 -> none; 1..12 -> level (ai-1)%4 with multiple {1,2,5}[(ai-1)/4]
+        if (ai > 0) {
+            const int lvl = (ai - 1) & 3, mul = (ai - 1) >> 2;
+            q[lvl] = wmul(mul == 0 ? 1 : (mul == 1 ? 2 : 5), fq);
+        }
+        const i32 tot = wadd(wadd(q[0], q[1]), wadd(q[2], q[3]));
+        if (!(tot <= left)) { q[0] = f2i(floorf(i2f(left))); q[1] = q[2] = q[3] = 0; }
+        for (int k = 0; k < 4; ++k) put_row(lds_rows, row + k, 1, side, q[k], pl[k], c.placeholder_order_id, tid, ta, tb);
+        return;
+    }
+    if (tc.action_space == HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG) {  // one row at [0, FT, M, NT, PP][a]
+        const int ai = action < 0 ? imax_(action + 5, 0) : (action > 4 ? 4 : action);
+        const i32 p = ai == 0 ? 0 : pl[ai - 1];
+        i32 qq = ai == 0 ? 0 : fq;
+        qq = qq <= left ? qq : 0;
+        put_row(lds_rows, row, 1, side, qq, p, c.placeholder_order_id, tid, ta, tb);
+        return;
+    }
+    // two rows at (FT, NT)
+    const i32 ft = sell ? bb : ba, nt = sell ? ba : bb;
+    if (tc.action_space == HFTLOB_EXE_ACT_SIMPLEST_CASE) {
+        const int ai = action < 0 ? imax_(action + 3, 0) : (action > 2 ? 2 : action);
+        q[0] = ai == 1 ? fq : 0;
+        q[1] = ai == 2 ? fq : 0;
+        if (!(wadd(q[0], q[1]) <= left)) { q[0] = f2i(floorf(i2f(wmul(fq, left)))); q[1] = 0; }
+    } else {  // twap: ceil(max(task - executed, 0) / steps_left) at FT (action 0) or NT (action 1)
+        const int ai = action < 0 ? imax_(action + 2, 0) : (action > 1 ? 1 : action);
+        const i32 steps_left = wsub(wsub(max_steps, step), 1);
+        const i32 qts = f2i_sat(ceilf(i2f(imax_(left, 0)) / i2f(steps_left)));
+        q[0] = ai == 0 ? qts : 0;
+        q[1] = ai == 1 ? qts : 0;
+    }
+    put_row(lds_rows, row, 1, side, q[0], ft, c.placeholder_order_id, tid, ta, tb);
+    put_row(lds_rows, row + 1, 1, side, q[1], nt, c.placeholder_order_id, tid, ta, tb);
 }
 
 // --------------------------------------------------------------- rewards
@@ -1941,7 +1986,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                     cancel_rows(B.a, R, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
                     STAMP_ACC(acc_cnl, ta1);
                 } else {
-                    exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow);
+                    exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, max_steps, rows, arow);
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
                     const i32 sell = s4[3];
@@ -1957,8 +2002,9 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                     for (int k = 0; k < 6; ++k) if (l == k) v = xv[k];
                     if (l < 6) axs[ag * 6 + l] = v;
                 }
-                if (tc.kind == HFTLOB_AGENT_MM) filter_rows<2>(rows, arow, crow, B.a.scr);
-                else filter_rows<4>(rows, arow, crow, B.a.scr);
+                if (tc.n_action_msgs == 2) filter_rows<2>(rows, arow, crow, B.a.scr);
+                else if (tc.n_action_msgs == 4) filter_rows<4>(rows, arow, crow, B.a.scr);
+                else filter_rows<1>(rows, arow, crow, B.a.scr);
                 STAMP_ACC(acc_flt, ta2);
                 arow += tc.n_action_msgs;
                 crow += tc.n_msgs - tc.n_action_msgs;
@@ -2291,7 +2337,13 @@ static int check_env(const hftlob_env_cfg* c) {
                 return fail(HFTLOB_EINVAL, "bob_v0 must be positive");
             if (tc.n_action_msgs != 2 || tc.n_msgs != 4) return fail(HFTLOB_EINVAL, "MM message counts");
         } else if (tc.kind == HFTLOB_AGENT_EXE) {
-            if (tc.n_action_msgs != 4 || tc.n_msgs != 8) return fail(HFTLOB_EINVAL, "EXE message counts");
+            const int a = tc.action_space;
+            const int na = a == HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX ? 4 : (a == HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG ? 1 : 2);
+            if (a < 0 || a > HFTLOB_EXE_ACT_TWAP) return fail(HFTLOB_EINVAL, "EXE action_space");
+            if (tc.n_action_msgs != na || tc.n_msgs != 2 * na) return fail(HFTLOB_EINVAL, "EXE message counts");
+            if (a == HFTLOB_EXE_ACT_TWAP && c->ep_type != 0) return fail(HFTLOB_EINVAL, "twap needs fixed_steps");
+            if (tc.observation_space < 0 || tc.observation_space > HFTLOB_EXE_OBS_SIMPLEST_CASE)
+                return fail(HFTLOB_EINVAL, "EXE observation_space");
         } else return fail(HFTLOB_EINVAL, "unknown agent kind");
     }
     if (agents != c->n_agents) return fail(HFTLOB_EINVAL, "n_agents mismatch");

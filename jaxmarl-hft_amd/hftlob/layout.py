@@ -83,8 +83,8 @@ MM_REWARD = {"portfolio_value": 0, "buy_sell_pnl": 1, "complex": 2, "zero_inv": 
              "spooner_scaled": 8, "delta_portfolio_value": 9}
 PRICE = {"mid": 0, "mid_avg": 1, "far_touch": 2, "near_touch": 3}
 INV_PEN = {"none": 0, "linear": 1, "quadratic": 2, "threshold": 3}
-EXE_ACTION = {"fixed_quants_complex": 0}
-EXE_OBS = {"engineered": 0}
+EXE_ACTION = {"fixed_quants_complex": 0, "simplest_case": 1, "fixed_quants_1msg": 2, "twap": 3}
+EXE_OBS = {"engineered": 0, "basic": 1, "simplest_case": 2}
 EXE_REWARD = {"normal": 0, "finish_fast": 1}
 TASK = {"random": 0, "buy": 1, "sell": 2}
 
@@ -125,7 +125,8 @@ def obs_dim(agent_cfg, world) -> int:
         raise ValueError(f"ep_type {world.ep_type!r}: use 'fixed_steps' or 'fixed_time'")
     if isinstance(agent_cfg, MarketMaking_EnvironmentConfig):
         return {"basic": 2, "engineered": 8}[agent_cfg.observation_space]
-    return {"engineered": 12 if world.ep_type == "fixed_steps" else 15}[agent_cfg.observation_space]
+    return {"engineered": 12 if world.ep_type == "fixed_steps" else 15, "basic": 3,
+            "simplest_case": 3}[agent_cfg.observation_space]
 
 
 @dataclass
@@ -248,8 +249,20 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
             a.avst_log_term[i] = float(np.float32(math.log(float(np.float32(np.float32(1.0) + q)))))
     else:
         a.kind = AGENT_EXE
+        if t.action_space == "fixed_quants":
+            raise NotImplementedError("EXE action_space 'fixed_quants': the reference's _getActionMsgs_fixedQuant "
+                                      "returns a bare array that get_messages unpacks into two values "
+                                      "(exec_env.py:727,1239-1244)")
+        if t.action_space == "fixed_prices":
+            raise NotImplementedError("EXE action_space 'fixed_prices' takes a Box action vector per agent; the "
+                                      "batched action buffer of the C ABI is one Discrete int per agent")
         if t.action_space not in EXE_ACTION:
-            raise NotImplementedError(f"EXE action_space {t.action_space!r} not implemented on the HIP path")
+            raise ValueError("Invalid action_space specified.")
+        if t.action_space == "fixed_quants_1msg" and t.larger_far_touch_quant:
+            raise NotImplementedError("fixed_quants_1msg with larger_far_touch_quant: Python `and` on a traced "
+                                      "action in the reference (exec_env.py:801)")
+        if t.action_space == "twap" and world.ep_type != "fixed_steps":
+            raise NotImplementedError("TWAP not implemented for fixed time episodes (exec_env.py:1141-1142)")
         if t.observation_space not in EXE_OBS:
             raise NotImplementedError(f"EXE observation_space {t.observation_space!r} not implemented")
         if t.reward_function not in EXE_REWARD:

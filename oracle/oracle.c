@@ -63,6 +63,20 @@ static inline float ffloordiv(float x, float y) {
 }
 static inline float i2f(i32 a) { return (float)a; }
 static inline i32 f2i(float f) { return (i32)f; } /* XLA convert: truncation */
+
+/* XLA f32 -> s32 convert (saturating; NaN -> 0) */
+static i32 f2i_sat(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f <= -2147483648.0f) return INT32_MIN;
+    return (i32)f;
+}
+/* jnp table[idx] on a traced index: negative indices wrap once, then clamp */
+static int gather_idx(i32 a, int n) {
+    i32 i = a < 0 ? a + n : a;
+    return i < 0 ? 0 : (i >= n ? n - 1 : i);
+}
+
 static inline float bitf(i32 w) { float f; memcpy(&f, &w, 4); return f; }
 static inline i32 fbit(float f) { i32 w; memcpy(&w, &f, 4); return w; }
 
@@ -534,7 +548,7 @@ static void mm_fixed_quant(const hftlob_env_cfg* c, const hftlob_agent_type_cfg*
     if (empty) { bb = BBIDS(E)[(c->n_msgs - 1) * 2]; ba = BASKS(E)[(c->n_msgs - 1) * 2]; }
     float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
     float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
-    int ai = action < 0 ? 0 : (action > 9 ? 9 : action); /* XLA gather clamps */
+    int ai = gather_idx(action, 10); /* jnp gather: negative wraps, then clamps */
     float bo = boff[ai], ao = aoff[ai];
     i32 bquant = wmul(bq[ai], tc->fixed_quant_value), aquant = wmul(aq[ai], tc->fixed_quant_value);
     if (empty) { bquant = 0; aquant = 0; }
@@ -561,19 +575,6 @@ static void mm_fixed_quant(const hftlob_env_cfg* c, const hftlob_agent_type_cfg*
     }
     x->bid_price = bp; x->ask_price = ap; x->bid_dist = wsub(bb, bp); x->ask_dist = wsub(ap, ba);
     x->bid_quant = bquant; x->ask_quant = aquant; x->empty_book = empty;
-}
-
-/* XLA f32 -> s32 convert (saturating; NaN -> 0) */
-static i32 f2i_sat(float f) {
-    if (f != f) return 0;
-    if (f >= 2147483648.0f) return INT32_MAX;
-    if (f <= -2147483648.0f) return INT32_MIN;
-    return (i32)f;
-}
-/* jnp table[idx] on a traced index: negative indices wrap once, then clamp */
-static int gather_idx(i32 a, int n) {
-    i32 i = a < 0 ? a + n : a;
-    return i < 0 ? 0 : (i >= n ? n - 1 : i);
 }
 
 /* MM bobRL (:1474-1561), bobStrategy (:1400-1472), AvSt (:1248-1398),
@@ -692,7 +693,7 @@ static void mm_directional(const hftlob_env_cfg* c, const hftlob_agent_type_cfg*
     i32 tick = c->tick_size;
     i32 ba = wmul(ifloordiv(BASKS(E)[(c->n_msgs - 1) * 2], tick), tick);
     i32 bb = wmul(ifloordiv(BBIDS(E)[(c->n_msgs - 1) * 2], tick), tick);
-    int ai = action < 0 ? 0 : (action > 2 ? 2 : action);
+    int ai = gather_idx(action, 3);
     i32 bq = (ai == 1) * tc->fixed_quant_value, aq = (ai == 2) * tc->fixed_quant_value;
     i32 q[2] = {bq, aq}, p[2] = {ba, bb}, sd[2] = {1, -1};
     const i32* wt = WORLD(E);
@@ -727,16 +728,53 @@ static void exe_fqc(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, En
         pl[2] = bb;
         pl[3] = wsub(bb, wmul(tick, tc->n_ticks_in_book));
     }
-    int ai = action < 0 ? 0 : (action > 12 ? 12 : action);
-    i32 q[4], tot = 0;
-    for (int k = 0; k < 4; ++k) { q[k] = wmul(QA[ai][k], tc->fixed_quant_value); tot = wadd(tot, q[k]); }
-    i32 left = wsub(st[1], st[2]);
-    if (!(tot <= left)) { q[0] = f2i(floorf(i2f(left))); q[1] = q[2] = q[3] = 0; }
+    i32 fq = tc->fixed_quant_value, left = wsub(st[1], st[2]);
+    i32 q[4] = {0, 0, 0, 0}, p[4] = {pl[0], pl[1], pl[2], pl[3]};
+    int n = 4;
+    switch (tc->action_space) {
+        case HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX: { /* :838-933 */
+            int ai = gather_idx(action, 13);
+            i32 tot = 0;
+            for (int k = 0; k < 4; ++k) { q[k] = wmul(QA[ai][k], fq); tot = wadd(tot, q[k]); }
+            if (!(tot <= left)) { q[0] = f2i(floorf(i2f(left))); q[1] = q[2] = q[3] = 0; }
+            break;
+        }
+        case HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG: { /* :732-836: one message */
+            static const i32 QN[5] = {0, 1, 1, 1, 1};
+            int ai = gather_idx(action, 5);
+            i32 prices[5] = {0, pl[0], pl[1], pl[2], pl[3]};
+            i32 sq = wmul(QN[ai], fq);
+            q[0] = sq <= left ? sq : 0;
+            p[0] = prices[ai];
+            n = 1;
+            break;
+        }
+        case HFTLOB_EXE_ACT_SIMPLEST_CASE: { /* :935-999: (FT, NT) */
+            int ai = gather_idx(action, 3);
+            i32 QS[3][2] = {{0, 0}, {fq, 0}, {0, fq}};
+            q[0] = QS[ai][0]; q[1] = QS[ai][1];
+            if (!(wadd(q[0], q[1]) <= left)) { q[0] = f2i(floorf(i2f(wmul(QS[1][0], left)))); q[1] = 0; }
+            p[0] = sell ? bb : ba; p[1] = sell ? ba : bb;
+            n = 2;
+            break;
+        }
+        default: { /* twap :1126-1227 (fixed_steps): ceil(max(left, 0) / steps_left) */
+            static const i32 QT[2][2] = {{1, 0}, {0, 1}};
+            const i32* L = LOADED(E);
+            i32 steps_left = wsub(wsub(L[3], L[5]), 1);
+            i32 qts = f2i_sat(ceilf(i2f(imax(left, 0)) / i2f(steps_left)));
+            int ai = gather_idx(action, 2);
+            q[0] = wmul(QT[ai][0], qts); q[1] = wmul(QT[ai][1], qts);
+            p[0] = sell ? bb : ba; p[1] = sell ? ba : bb;
+            n = 2;
+            break;
+        }
+    }
     i32 side = wsub(1, wmul(sell, 2));
     const i32* wt = WORLD(E);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < n; ++k) {
         i32* o = out + k * 8;
-        o[0] = 1; o[1] = side; o[2] = q[k]; o[3] = pl[k]; o[4] = c->placeholder_order_id; o[5] = tid;
+        o[0] = 1; o[1] = side; o[2] = q[k]; o[3] = p[k]; o[4] = c->placeholder_order_id; o[5] = tid;
         o[6] = wadd(wt[0], tc->time_delay_obs_act); o[7] = wadd(wt[1], tc->time_delay_obs_act);
     }
 }
@@ -1061,6 +1099,37 @@ static void mm_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env
 /* EXE _get_obs — exec_env.py:1913-2079; sorted keys (fixed_steps 12, fixed_time 15) */
 static void exe_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env* E, const i32* st, float* o) {
     int M = c->n_msgs, nO = c->lob.n_orders, nz = tc->normalize;
+    if (tc->observation_space == HFTLOB_EXE_OBS_BASIC) {
+        /* _get_obs_basic :1879-1911; sorted keys best_ask_price, best_bid_price, remaining_quant */
+        i32 a = BASKS(E)[(M - 1) * 2], b = BBIDS(E)[(M - 1) * 2], rq = wsub(st[1], st[2]);
+        if (nz) {
+            o[0] = i2f(wsub(a, 1550000)) / 1e3f;
+            o[1] = i2f(wsub(b, 1550000)) / 1e3f;
+            o[2] = i2f(rq) / (float)tc->task_size;
+        } else {
+            o[0] = i2f(a); o[1] = i2f(b); o[2] = i2f(rq);
+        }
+        return;
+    }
+    if (tc->observation_space == HFTLOB_EXE_OBS_SIMPLEST_CASE) {
+        /* _get_obs_simplest_case :1841-1877; sorted keys mid_price, percent_remaining_quant,
+         * percent_time_remaining */
+        const i32* W = WORLD(E);
+        const i32* L = LOADED(E);
+        i32 tu0 = wsub(W[0], L[0]), tu1 = wsub(W[1], L[1]);
+        float ep = (float)c->episode_time;
+        float ptr = (ep - (i2f(tu0) + i2f(tu1) / 1e9f)) / ep;
+        float prq = i2f(wsub(st[1], st[2])) / i2f(st[1]);
+        float mid = bitf(W[3]);
+        if (nz) {
+            o[0] = (mid - 7560000.0f) / 1e3f;
+            o[1] = (prq - 0.5f) / 1.0f;
+            o[2] = (ptr - 0.5f) / 1.0f;
+        } else {
+            o[0] = mid; o[1] = prq; o[2] = ptr;
+        }
+        return;
+    }
     i32 sell = st[3];
     i32 pa = BASKS(E)[(M - 1) * 2], pb = BBIDS(E)[(M - 1) * 2];
     i32 p_aggr = sell ? pb : pa, p_pass = sell ? pa : pb;
@@ -1422,7 +1491,16 @@ void oracle_split_keys(int n_env, int n, int part, const u32* keys, u32* out) {
  * ask_quant, empty_book. */
 int oracle_mm_action_msgs(const hftlob_env_cfg* c, int type, int agent, const i32* rec, i32 action, i32* out,
                           i32* extras) {
-    if (type < 0 || type >= c->n_types || c->types[type].kind != HFTLOB_AGENT_MM) return HFTLOB_EINVAL;
+    if (type < 0 || type >= c->n_types) return HFTLOB_EINVAL;
+    if (c->types[type].kind == HFTLOB_AGENT_EXE) { /* EXE: up to 4 rows, no extras */
+        const hftlob_agent_type_cfg* te = &c->types[type];
+        int off = c->off_agents;
+        for (int t = 0; t < type; ++t) off += c->types[t].n_agents * agent_words(&c->types[t]);
+        Env E = {c, (i32*)rec};
+        exe_fqc(c, te, &E, rec + off + agent * agent_words(te), wsub(te->trader_id0, agent), action, out);
+        memset(extras, 0, 7 * sizeof(i32));
+        return HFTLOB_OK;
+    }
     const hftlob_agent_type_cfg* tc = &c->types[type];
     Env E = {c, (i32*)rec};
     int a0 = 0, off = c->off_agents;

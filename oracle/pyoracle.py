@@ -122,12 +122,13 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
 
 
 def mm_action_msgs(env_cfg, type_idx, agent, rec, action):
-    """(rows int32 [2, 8], extras [7]) of one MM agent's raw action messages for record `rec`."""
-    out = np.zeros((2, 8), np.int32)
+    """(rows int32 [n_action_msgs, 8], extras [7]) of one agent's raw action messages for record `rec`
+    (MM: 2 rows + extras; EXE: n_action_msgs rows)."""
+    out = np.zeros((4, 8), np.int32)
     ex = np.zeros(7, np.int32)
     rec = np.ascontiguousarray(rec, dtype=np.int32)
     _chk(lib().oracle_mm_action_msgs(C.byref(env_cfg), type_idx, agent, _p(rec), int(action), _p(out), _p(ex)))
-    return out, ex
+    return out[:env_cfg.types[type_idx].n_action_msgs], ex
 
 
 def sample_actions(env_cfg, keys):

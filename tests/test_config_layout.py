@@ -67,7 +67,9 @@ def test_roundtrip(tmp_path, fmt):
     ("MarketMaking", dict(action_space="bobRL", sell_buy_all_option=True), NotImplementedError),
     ("MarketMaking", dict(reward_function="bogus"), ValueError),
     ("MarketMaking", dict(unwind_price="near_touch"), ValueError),
-    ("Execution", dict(action_space="twap"), NotImplementedError),
+    ("Execution", dict(action_space="fixed_quants"), NotImplementedError),   # reference unpack error
+    ("Execution", dict(action_space="fixed_prices"), NotImplementedError),   # Box actions
+    ("Execution", dict(action_space="fixed_quants_1msg", larger_far_touch_quant=True), NotImplementedError),
     ("Execution", dict(reference_price="near_touch"), ValueError),
 ])
 def test_unsupported_options_fail_loudly(agent, changes, err):
@@ -90,6 +92,7 @@ def test_cancel_mode_values():
 
 
 REF_CFG_DIR = "/root/reference/config/env_configs"
+GAP_CONFIGS = {"exec_debug_fixed_price.json", "exec_longrun_fixed_price.json"}
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_CFG_DIR), reason="reference configs not mounted")
@@ -100,7 +103,8 @@ def test_reference_env_configs_pack(fname):
     cfg = load_config_from_file(os.path.join(REF_CFG_DIR, fname))
     try:
         c, L = pack_env_cfg(cfg, 4, 100_000, True)
-    except NotImplementedError as e:       # documented gaps only (EXE variants, MM fixed_prices)
-        assert "not implemented" in str(e) or "NameError" in str(e)
+    except NotImplementedError as e:       # documented gap: EXE fixed_prices (Box actions)
+        assert fname in GAP_CONFIGS and "fixed_prices" in str(e), (fname, str(e))
         return
+    assert fname not in GAP_CONFIGS
     assert c.n_msgs == L.n_msgs and c.n_types == len(cfg.dict_of_agents_configs)

@@ -215,7 +215,12 @@ def test_mm_avst_fixed_time(tmp_path_factory):
 EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid", task="buy"),
                 dict(task="sell", normalize=False),
                 dict(doom_price_penalty=0.1),                    # Python-float penalty: f32 far-touch price
-                dict(doom_price_penalty=0.37, reference_price="mid")]
+                dict(doom_price_penalty=0.37, reference_price="mid"),
+                dict(action_space="simplest_case"), dict(action_space="simplest_case", task_size=25),
+                dict(action_space="fixed_quants_1msg"), dict(action_space="fixed_quants_1msg", task_size=40),
+                dict(action_space="twap"), dict(action_space="twap", task_size=7, task="buy"),
+                dict(observation_space="basic"), dict(observation_space="basic", normalize=False),
+                dict(observation_space="simplest_case"), dict(observation_space="simplest_case", normalize=False)]
 
 
 @pytest.mark.parametrize("changes", EXE_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
