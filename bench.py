@@ -9,6 +9,11 @@
   the unfused three-launch form is checked bit-exact against it in
   tests/test_gpu_env.py.
 
+Launches: K eager launches back to back on one stream (--graph-steps G > 0
+replays a captured HIP graph of G launches instead; it measures the same on
+MI355X, since a 116 us kernel hides the host launch cost).  roofline.kernel_ms
+is the HIP-event time of the timed region on the launch stream / K.
+
 Weak scaling: every rank (one process per GPU) steps its own 4096 envs on a
 replicated synthetic LOBSTER day; no collective on the data path (only the
 timing barrier / max-over-ranks).  Prints ONE JSON line on rank 0.
@@ -73,6 +78,8 @@ def main():
     ap.add_argument("--n-msgs", type=int, default=400_000, help="synthetic day length (messages)")
     ap.add_argument("--mid", type=int, default=2_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps per captured HIP graph in the timed region (even; 0 = eager launches)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
@@ -110,29 +117,50 @@ def main():
     kbuf = [torch.tensor([0, 1 + rank], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
     nstep = [0]
 
-    def one_step(ev=None):
+    def one_step():
         k = nstep[0]
-        if ev is not None:
-            ev[0].record()
         env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)
-        if ev is not None:
-            ev[1].record()
         nstep[0] = k + 1
 
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
+    G = args.graph_steps if args.graph_steps > 0 and args.graph_steps % 2 == 0 else 0
+    graph = None
+    if G:
+        # G consecutive launches in one HIP graph; G is even, so the key ping-pong buffers line up
+        # between replays (every launch's pointers are baked in at capture)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            one_step()
+            one_step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(G):
+                one_step()
+        graph.replay()                        # one untimed replay (graph upload)
+        torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     D.barrier(R)
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize()
     D.barrier(R)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        one_step(events[k])
+    ev0.record()                              # on the launch stream (torch's current stream)
+    done = 0
+    if graph is not None:
+        for _ in range(args.steps // G):
+            graph.replay()
+        done = args.steps // G * G
+    for _ in range(args.steps - done):
+        one_step()
+    ev1.record()
     torch.cuda.synchronize()
     D.barrier(R)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in events) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / args.steps   # average k_env_step launch duration, HIP events
     elapsed = D.max_over_ranks(R, elapsed, device="cuda")
 
     if rank != 0:
@@ -169,7 +197,8 @@ def main():
         "data": f"synthetic LOBSTER day ({args.n_msgs} msgs, PCG64 seed 20260403, mid {args.mid})",
         "config": {"workload": f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, 112 msgs/step, "
                                f"auto-reset, Speed_test rollout semantics",
-                   "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)"},
+                   "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)",
+                   "launch": f"hipGraph of {G} steps" if G else "eager"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                      "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env},
