@@ -1,0 +1,308 @@
+"""IPPO with recurrent actor-critics, trained against the HIP env step (the
+reference's consumer loop, gymnax_exchange/jaxrl/MARL/ippo_rnn_JAXMARL.py).
+
+One network (and optimizer) per agent type, as the reference:
+
+* ``ActorCriticRNN`` (:203-256): Dense(FC_DIM_SIZE, orthogonal sqrt 2) + relu ->
+  GRU(GRU_HIDDEN_DIM) whose carry is zeroed where the actor's previous done is set
+  (ScannedRNN, :53-78) -> critic Dense(FC)+relu+Dense(1) and actor
+  Dense(GRU_HIDDEN_DIM)+relu+Dense(n_actions, orthogonal 0.01) categorical head
+  (SingleActionOutput :183-201).
+* rollout (:578-663): NUM_STEPS steps of sample -> env.step, the transitions kept
+  in preallocated device buffers (no host synchronisation inside the rollout);
+  actors are (env, agent) pairs of one type, ``batchify`` order.
+* GAE (:668-690) with the per-type GAMMA / GAE_LAMBDA and the env's global done.
+* PPO update (:711-838): UPDATE_EPOCHS x NUM_MINIBATCHES over a permutation of
+  the actors (whole sequences, the GRU is re-run from the rollout's initial carry);
+  clipped value loss, clipped surrogate with per-minibatch advantage
+  normalisation, entropy bonus; Adam(eps 1e-5) after global-norm clipping, linear
+  LR annealing by update count.
+* multi-GPU (ippo_rnn_JAXMARL_pmap.py:566-567 pmean of grads): every rank steps
+  its own env shard; gradients are averaged with one all-reduce per agent type
+  and minibatch (``torch.distributed``, RCCL on ROCm).
+
+Differences that are not semantics of the env: action sampling and parameter
+initialisation draw from torch's generator, not JAX's threefry, and the network
+runs through torch (rocBLAS GEMMs) rather than XLA.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..env import MARLEnv, split_keys
+
+
+def _per_type(v, n: int) -> list:
+    """A per-agent-type hyper-parameter list of length n (a scalar or a shorter list repeats its last value)."""
+    v = list(v) if isinstance(v, (list, tuple)) else [v]
+    return (v + [v[-1]] * n)[:n]
+
+
+def default_config(**kw) -> Dict:
+    """The reference's ippo_rnn_JAXMARL_2player.yaml hyper-parameters (training keys only)."""
+    c = {"LR": [2.5e-4, 2.5e-4], "NUM_ENVS": 4096, "NUM_STEPS": 64, "GRU_HIDDEN_DIM": 256, "FC_DIM_SIZE": 256,
+         "TOTAL_TIMESTEPS": 5e8, "UPDATE_EPOCHS": 4, "NUM_MINIBATCHES": 4, "GAMMA": [0.999999999, 0.999],
+         "GAE_LAMBDA": [0.85, 0.9], "CLIP_EPS": 0.2, "ENT_COEF": [0.01, 0.01], "VF_COEF": [0.5, 0.5],
+         "MAX_GRAD_NORM": [0.5, 0.5], "ANNEAL_LR": [True, True], "NUM_AGENTS_PER_TYPE": [1, 1], "SEED": 2}
+    c.update(kw)
+    return c
+
+
+class ActorCriticRNN(nn.Module):
+    def __init__(self, obs_dim: int, n_actions: int, fc: int, hidden: int):
+        super().__init__()
+        self.embed = nn.Linear(obs_dim, fc)
+        self.gru = nn.GRUCell(fc, hidden)
+        self.critic1, self.critic2 = nn.Linear(hidden, fc), nn.Linear(fc, 1)
+        self.actor1, self.actor2 = nn.Linear(hidden, hidden), nn.Linear(hidden, n_actions)
+        for m, g in ((self.embed, math.sqrt(2)), (self.critic1, 2.0), (self.critic2, 1.0), (self.actor1, 2.0),
+                     (self.actor2, 0.01)):
+            nn.init.orthogonal_(m.weight, g)
+            nn.init.zeros_(m.bias)
+        self.hidden = hidden
+
+    def step(self, h: torch.Tensor, obs: torch.Tensor, done: torch.Tensor):
+        """One time step for a batch of actors: (new carry, logits, value)."""
+        h = torch.where(done[:, None], torch.zeros_like(h), h)
+        h = self.gru(F.relu(self.embed(obs)), h)
+        v = self.critic2(F.relu(self.critic1(h))).squeeze(-1)
+        return h, self.actor2(F.relu(self.actor1(h))), v
+
+    def forward(self, h0: torch.Tensor, obs: torch.Tensor, dones: torch.Tensor):
+        """A sequence [T, B, ...] from carry h0 (the ScannedRNN scan): logits [T, B, A], values [T, B]."""
+        logits, values = [], []
+        h = h0
+        for t in range(obs.shape[0]):
+            h, lg, v = self.step(h, obs[t], dones[t])
+            logits.append(lg)
+            values.append(v)
+        return torch.stack(logits), torch.stack(values)
+
+
+@dataclass
+class Rollout:
+    """One agent type's trajectory buffers, [T, n_actors, ...] on the device."""
+    obs: torch.Tensor
+    done: torch.Tensor          # the actor's done entering the step (GRU reset)
+    global_done: torch.Tensor   # dones["__all__"] of the env (GAE)
+    action: torch.Tensor
+    value: torch.Tensor
+    reward: torch.Tensor
+    log_prob: torch.Tensor
+
+
+def calculate_gae(reward, value, global_done, last_val, gamma: float, lam: float):
+    """_calculate_gae (:668-690): reverse scan; returns (advantages, targets)."""
+    T = reward.shape[0]
+    adv = torch.empty_like(reward)
+    gae = torch.zeros_like(last_val)
+    next_value = last_val
+    for t in range(T - 1, -1, -1):
+        nd = 1.0 - global_done[t].to(reward.dtype)
+        delta = reward[t] + gamma * next_value * nd - value[t]
+        gae = delta + gamma * lam * nd * gae
+        adv[t] = gae
+        next_value = value[t]
+    return adv, adv + value
+
+
+def ppo_loss(logits, values, rb_action, rb_value, rb_log_prob, gae, targets, clip_eps: float, vf_coef: float,
+             ent_coef: float):
+    """_loss_fn (:718-765) -> (total, value_loss, actor_loss, entropy, approx_kl, clip_frac)."""
+    logp_all = F.log_softmax(logits, -1)
+    log_prob = logp_all.gather(-1, rb_action.long().unsqueeze(-1)).squeeze(-1)
+    v_clip = rb_value + (values - rb_value).clamp(-clip_eps, clip_eps)
+    value_loss = 0.5 * torch.maximum((values - targets) ** 2, (v_clip - targets) ** 2).mean()
+    logratio = log_prob - rb_log_prob
+    ratio = torch.exp(logratio)
+    gae = (gae - gae.mean()) / (gae.std(unbiased=False) + 1e-8)
+    actor_loss = -torch.minimum(ratio * gae, ratio.clamp(1.0 - clip_eps, 1.0 + clip_eps) * gae).mean()
+    entropy = -(logp_all.exp() * logp_all).sum(-1).mean()
+    approx_kl = ((ratio - 1) - logratio).mean()
+    clip_frac = ((ratio - 1).abs() > clip_eps).float().mean()
+    total = actor_loss + vf_coef * value_loss - ent_coef * entropy
+    return total, value_loss, actor_loss, entropy, approx_kl, clip_frac
+
+
+def linear_schedule(lr: float, count: int, n_minibatches: int, n_epochs: int, n_updates: int) -> float:
+    """linear_schedule (:503-509): lr * (1 - (count // (minibatches * epochs)) / NUM_UPDATES)."""
+    return lr * (1.0 - (count // (n_minibatches * n_epochs)) / n_updates)
+
+
+def _average_grads(params, dist) -> None:
+    """pmean of the gradients over ranks: one flattened all-reduce (bucket) per call."""
+    grads = [p.grad for p in params if p.grad is not None]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat)
+    flat /= dist.get_world_size()
+    o = 0
+    for g in grads:
+        g.copy_(flat[o:o + g.numel()].view_as(g))
+        o += g.numel()
+
+
+class IPPOTrainer:
+    """make_train(config)(rng) of the reference, one ``update`` per call."""
+
+    def __init__(self, env: MARLEnv, config: Dict, dist=None, device=None):
+        self.env, self.c, self.dist = env, config, dist
+        self.device = torch.device(device or env.device)
+        nt = len(env.list_of_agents_configs)
+        self.n_types = nt
+        c = config
+        for k in ("LR", "GAMMA", "GAE_LAMBDA", "ENT_COEF", "VF_COEF", "MAX_GRAD_NORM", "ANNEAL_LR"):
+            c[k] = _per_type(c[k], nt)
+        self.E, self.T = c["NUM_ENVS"], c["NUM_STEPS"]
+        self.n_agents = list(env.multi_agent_config.number_of_agents_per_type)
+        self.n_actors = [n * self.E for n in self.n_agents]
+        world = dist.get_world_size() if dist is not None else 1
+        self.num_updates = max(1, int(c["TOTAL_TIMESTEPS"] // self.T // (self.E * world)))
+        torch.manual_seed(c["SEED"])  # the same initial parameters on every rank
+        self.nets = [ActorCriticRNN(env.observation_spaces[i].shape[0], env.action_spaces[i].n, c["FC_DIM_SIZE"],
+                                    c["GRU_HIDDEN_DIM"]).to(self.device) for i in range(nt)]
+        self.opts = [torch.optim.Adam(n.parameters(), lr=c["LR"][i], eps=1e-5) for i, n in enumerate(self.nets)]
+        self.opt_count = [0] * nt
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(c["SEED"] + 1000 * (dist.get_rank() if dist is not None else 0))
+        self.params = env.default_params
+        self._split = getattr(env, "split_keys", split_keys)   # device threefry split (jax.random.split)
+        rank = dist.get_rank() if dist is not None else 0
+        master = torch.tensor([[c["SEED"], rank]], dtype=torch.int32, device=self.device)
+        k = self._split(master, 2)[0]
+        self.rng = k[0].clone()
+        reset_keys = self._split(k[1:2].contiguous(), self.E)[0].contiguous()
+        obs, self.state = env.reset(reset_keys, self.params)
+        self.last_obs = [o.reshape(n, -1).clone() for o, n in zip(obs, self.n_actors)]
+        self.last_done = [torch.zeros(n, dtype=torch.bool, device=self.device) for n in self.n_actors]
+        self.h = [torch.zeros(n, c["GRU_HIDDEN_DIM"], device=self.device) for n in self.n_actors]
+        T = self.T
+        self.buf = [Rollout(obs=torch.empty((T, n, env.observation_spaces[i].shape[0]), device=self.device),
+                            done=torch.empty((T, n), dtype=torch.bool, device=self.device),
+                            global_done=torch.empty((T, n), dtype=torch.bool, device=self.device),
+                            action=torch.empty((T, n), dtype=torch.int32, device=self.device),
+                            value=torch.empty((T, n), device=self.device),
+                            reward=torch.empty((T, n), device=self.device),
+                            log_prob=torch.empty((T, n), device=self.device))
+                    for i, n in enumerate(self.n_actors)]
+
+    def _next_keys(self) -> torch.Tensor:
+        """rng, _rng = split(rng); rng_step = split(_rng, NUM_ENVS) (:613-614)."""
+        k = self._split(self.rng[None], 2)[0]
+        self.rng = k[0].clone()
+        return self._split(k[1:2].contiguous(), self.E)[0].contiguous()
+
+    @torch.no_grad()
+    def rollout(self) -> None:
+        """NUM_STEPS of _env_step (:578-658), all on the device."""
+        for t in range(self.T):
+            actions = []
+            for i, net in enumerate(self.nets):
+                b = self.buf[i]
+                b.obs[t].copy_(self.last_obs[i])
+                b.done[t].copy_(self.last_done[i])
+                self.h[i], logits, v = net.step(self.h[i], self.last_obs[i], self.last_done[i])
+                probs = torch.softmax(logits, -1)
+                a = torch.multinomial(probs, 1, generator=self.gen).squeeze(-1)
+                b.action[t].copy_(a)
+                b.value[t].copy_(v)
+                b.log_prob[t].copy_(torch.log_softmax(logits, -1).gather(-1, a.unsqueeze(-1)).squeeze(-1))
+                actions.append(a.view(self.E, self.n_agents[i]))
+            obs, self.state, rew, dones, _ = self.env.step(self._next_keys(), self.state, actions, self.params)
+            for i in range(self.n_types):
+                b = self.buf[i]
+                b.reward[t].copy_(rew[i].reshape(-1))
+                b.global_done[t].copy_(dones["__all__"].repeat_interleave(self.n_agents[i]))
+                self.last_obs[i].copy_(obs[i].reshape(self.n_actors[i], -1))
+                self.last_done[i].copy_(dones["agents"][i].reshape(-1))
+
+    def update(self) -> Dict:
+        """One _update_step: rollout, GAE, UPDATE_EPOCHS x NUM_MINIBATCHES PPO steps per agent type."""
+        c = self.c
+        h0 = [h.clone() for h in self.h]
+        self.rollout()
+        metrics = {"loss": [], "avg_reward": []}
+        for i, net in enumerate(self.nets):
+            b = self.buf[i]
+            with torch.no_grad():
+                _, _, last_val = net.step(self.h[i], self.last_obs[i], self.last_done[i])
+                adv, targets = calculate_gae(b.reward, b.value, b.global_done, last_val, c["GAMMA"][i],
+                                             c["GAE_LAMBDA"][i])
+            n, mb = self.n_actors[i], c["NUM_MINIBATCHES"]
+            stats = torch.zeros(6, device=self.device)
+            for _ in range(c["UPDATE_EPOCHS"]):
+                perm = torch.randperm(n, device=self.device, generator=self.gen)
+                for idx in perm.view(mb, n // mb):
+                    if c["ANNEAL_LR"][i]:
+                        lr = linear_schedule(c["LR"][i], self.opt_count[i], mb, c["UPDATE_EPOCHS"], self.num_updates)
+                        for g in self.opts[i].param_groups:
+                            g["lr"] = lr
+                    logits, values = net(h0[i][idx], b.obs[:, idx], b.done[:, idx])
+                    out = ppo_loss(logits, values, b.action[:, idx], b.value[:, idx], b.log_prob[:, idx],
+                                   adv[:, idx], targets[:, idx], c["CLIP_EPS"], c["VF_COEF"][i], c["ENT_COEF"][i])
+                    self.opts[i].zero_grad(set_to_none=True)
+                    out[0].backward()
+                    if self.dist is not None and self.dist.get_world_size() > 1:
+                        _average_grads(list(net.parameters()), self.dist)
+                    torch.nn.utils.clip_grad_norm_(net.parameters(), c["MAX_GRAD_NORM"][i])
+                    self.opts[i].step()
+                    self.opt_count[i] += 1
+                    stats += torch.stack([x.detach() for x in out])
+            stats /= c["UPDATE_EPOCHS"] * mb
+            metrics["loss"].append(dict(zip(("total_loss", "value_loss", "actor_loss", "entropy", "approx_kl",
+                                             "clip_frac"), stats)))
+            metrics["avg_reward"].append(b.reward.mean())
+        return metrics
+
+
+def train(env: MARLEnv, config: Dict, n_updates: Optional[int] = None, dist=None, log=print):
+    """Runs ``n_updates`` (default NUM_UPDATES) updates; returns (trainer, env-steps/s over the run)."""
+    tr = IPPOTrainer(env, config, dist=dist)
+    n = n_updates or tr.num_updates
+    sync = torch.cuda.synchronize if tr.device.type == "cuda" else (lambda: None)
+    sync()
+    t0 = time.perf_counter()
+    for u in range(n):
+        m = tr.update()
+        if log is not None:
+            log({"update": u, "avg_reward": [float(r) for r in m["avg_reward"]],
+                 "loss": [{k: float(v) for k, v in d.items()} for d in m["loss"]]})
+    sync()
+    world = dist.get_world_size() if dist is not None else 1
+    return tr, n * tr.T * tr.E * world / (time.perf_counter() - t0)
+
+
+def main(argv=None) -> None:
+    """python -m hftlob.train.ippo [--rl-config ippo.yaml] [--env-config 2_player_fq_fqc] [--updates N]"""
+    import argparse
+    import json
+    import yaml
+    from ..config_io import builtin_config, load_config_from_file
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rl-config", default=None, help="reference-style YAML (ippo_rnn_JAXMARL_2player.yaml keys)")
+    ap.add_argument("--env-config", default="2_player_fq_fqc", help="JSON path or builtin config name")
+    ap.add_argument("--updates", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=None)
+    ap.add_argument("--data", default=None, help="'lobster' to load world_config.dataPath (else synthetic)")
+    a = ap.parse_args(argv)
+    c = default_config()
+    if a.rl_config:
+        with open(a.rl_config) as f:
+            c.update({k: v for k, v in yaml.safe_load(f).items() if k in c})
+    if a.envs:
+        c["NUM_ENVS"] = a.envs
+    cfg = (load_config_from_file(a.env_config) if a.env_config.endswith((".json", ".yaml"))
+           else builtin_config(a.env_config))
+    env = MARLEnv(None, cfg, data=a.data, return_info=False, persistent_outputs=True)
+    _, sps = train(env, c, a.updates, log=lambda m: print(json.dumps(m)))
+    print(json.dumps({"env_steps_per_s_incl_learner": sps, "num_envs": c["NUM_ENVS"], "num_steps": c["NUM_STEPS"]}))
+
+
+if __name__ == "__main__":
+    main()
