@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per captured HIP graph in the timed region (even; 0 = eager launches)")
+    ap.add_argument("--config", default=CONFIG, help="builtin env config (the metric: 2_player_fq_fqc)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
@@ -93,7 +94,7 @@ def main():
     from hftlob.env import MARLEnv, split_keys
     from hftlob import _lib
 
-    cfg = builtin_config(CONFIG)
+    cfg = builtin_config(args.config)
     w = cfg.world_config
     snap = w.n_data_msg_per_step * w.start_resolution
     cache = f"/tmp/hftlob_day_{args.n_msgs}_{args.mid}_{snap}.npz"
@@ -195,8 +196,9 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": f"synthetic LOBSTER day ({args.n_msgs} msgs, PCG64 seed 20260403, mid {args.mid})",
-        "config": {"workload": f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, 112 msgs/step, "
-                               f"auto-reset, Speed_test rollout semantics",
+        "config": {"workload": (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, 112 msgs/step, "
+                                f"auto-reset, Speed_test rollout semantics") if args.config == CONFIG else
+                               f"{args.config}.json, {env.num_msgs_per_step} msgs/step, auto-reset, Speed_test semantics",
                    "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)",
                    "launch": f"hipGraph of {G} steps" if G else "eager"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
