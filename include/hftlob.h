@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HFTLOB_ABI_VERSION 3
+#define HFTLOB_ABI_VERSION 4
 
 #define HFTLOB_OK            0
 #define HFTLOB_EINVAL      (-1)   /* bad config value / unsupported option */
@@ -78,7 +78,7 @@ enum { HFTLOB_PRICE_MID = 0, HFTLOB_PRICE_MID_AVG = 1, HFTLOB_PRICE_FAR_TOUCH = 
 enum { HFTLOB_INVPEN_NONE = 0, HFTLOB_INVPEN_LINEAR, HFTLOB_INVPEN_QUADRATIC,
        HFTLOB_INVPEN_THRESHOLD };
 enum { HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX = 0, HFTLOB_EXE_ACT_SIMPLEST_CASE = 1, HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG = 2,
-       HFTLOB_EXE_ACT_TWAP = 3 };
+       HFTLOB_EXE_ACT_TWAP = 3, HFTLOB_EXE_ACT_FIXED_PRICES = 4 };
 enum { HFTLOB_EXE_OBS_ENGINEERED = 0, HFTLOB_EXE_OBS_BASIC = 1, HFTLOB_EXE_OBS_SIMPLEST_CASE = 2 };
 enum { HFTLOB_EXE_REW_NORMAL = 0, HFTLOB_EXE_REW_FINISH_FAST = 1 };
 enum { HFTLOB_TASK_RANDOM = 0, HFTLOB_TASK_BUY = 1, HFTLOB_TASK_SELL = 2 };
@@ -143,6 +143,9 @@ typedef struct hftlob_agent_type_cfg {
        (a Python float: the far-touch price is then computed in f32, exec_env.py:1544,1569-1573) */
     int32_t doom_penalty_is_float;
     float   doom_penalty_f32;
+    /* action words per agent in the actions buffer: 1 for a Discrete space; n_actions (1..4) for
+       the EXE fixed_prices MultiDiscrete([fixed_quant_value] * n_actions) space (exec_env.py:2167-2171) */
+    int32_t action_width;
 } hftlob_agent_type_cfg;
 
 /*
@@ -194,7 +197,8 @@ typedef struct hftlob_env_cfg {
     int32_t off_asks, off_bids, off_trades, off_loaded;
     int32_t off_best_bids, off_best_asks, off_world, off_agents;
     int32_t info_words;            /* words per env in the optional info buffer */
-    int32_t _pad[2];
+    int32_t action_words;          /* sum_t n_agents_t * action_width_t: int32 words per env of actions */
+    int32_t _pad[1];
     hftlob_agent_type_cfg types[HFTLOB_MAX_TYPES];
 } hftlob_env_cfg;
 
@@ -245,7 +249,8 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint
 
 /* Batched MARLEnv.step with auto-reset — replaces
  * jax.vmap(env.step, in_axes=(0, 0, 0, None)): marl_env.py:775-804 (step_env
- * :211-709).  keys uint32 [n_env][2]; actions int32 [n_env][n_agents]. */
+ * :211-709).  keys uint32 [n_env][2]; actions int32 [n_env][action_words]: agent by agent in
+ * type order, action_width words each (== [n_env][n_agents] when every space is Discrete). */
 int hftlob_env_step(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint32_t* keys,
                     const int32_t* actions, const int32_t* msg_data, const int32_t* init_states,
                     int32_t* state, const hftlob_step_out* out /*[host] struct*/, void* stream);
@@ -265,7 +270,10 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, con
 /* Speed_test action sampling (Speed_test.py:166-177, gymnax Discrete.sample):
  * for env e with step key k_e,
  * sub = split(k_e, n_types); per type t, agent i:
- * actions[e][agent] = randint(split(sub[t], n_agents_t)[i], 0, n_actions_t). */
+ * actions[e][agent] = randint(split(sub[t], n_agents_t)[i], 0, n_actions_t), or for
+ * MultiDiscrete (from_JAXMARL/spaces.py:57-65) the action_width words
+ * randint(split(sub[t], n_agents_t)[i], (width,), 0, fixed_quant_value).
+ * actions int32 [n_env][action_words]. */
 int hftlob_sample_actions(const hftlob_env_cfg* cfg /*[host]*/, int n_env, const uint32_t* keys,
                           int32_t* actions, void* stream);
 

@@ -168,16 +168,24 @@ DEV u32 random_bits(Key k, int n, int i, bool part) {
     threefry(k.a, k.b, (u32)(i - half), (i < n) ? (u32)i : 0u, y0, y1);
     return y1;
 }
-// jax.random.randint(key, (), lo, hi), int32
-DEV i32 randint(Key k, i32 lo, i32 hi, bool part) {
+// jax.random.randint(key, (n,), lo, hi)[j], int32 (n = 1: the scalar draw)
+DEV i32 randint_vec(Key k, int n, int j, i32 lo, i32 hi, bool part) {
     Key k1 = split_key(k, 2, 0, part), k2 = split_key(k, 2, 1, part);
-    u32 hb = random_bits(k1, 1, 0, part), lb = random_bits(k2, 1, 0, part);
+    u32 hb = random_bits(k1, n, j, part), lb = random_bits(k2, n, j, part);
     u32 span = (hi <= lo) ? 1u : (u32)hi - (u32)lo;
     u32 mult = 65536u % span;
     mult = (mult * mult) % span;
     u32 off = ((hb % span) * mult + (lb % span)) % span;
     return (i32)((u32)lo + off);
 }
+// upper bound of the agent type's random action draw: Discrete(n_actions).sample, or
+// MultiDiscrete([fixed_quant_value] * n_actions).sample for EXE fixed_prices (exec_env.py:2167-2171)
+DEV i32 action_hi(const hftlob_agent_type_cfg& tc) {
+    return tc.kind == HFTLOB_AGENT_EXE && tc.action_space == HFTLOB_EXE_ACT_FIXED_PRICES ? tc.fixed_quant_value
+                                                                                         : tc.n_actions;
+}
+// jax.random.randint(key, (), lo, hi), int32
+DEV i32 randint(Key k, i32 lo, i32 hi, bool part) { return randint_vec(k, 1, 0, lo, hi, part); }
 
 // ------------------------------------------------------------ book tables
 // Every table of the book (ask side, bid side, trade log) lives in LDS as
@@ -1505,6 +1513,53 @@ DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
     put_row(lds_rows, row + 1, 1, side, q[1], nt, c.placeholder_order_id, tid, ta, tb);
 }
 
+// EXE _getActionMsgs_fixedPrice — exec_env.py:1001-1123.  act[0..w) is the
+// MultiDiscrete action, w = n_actions (1..4): the quantity at each of the first w
+// price levels of (FT, M, NT, PP) / (FT, NT, PP) / (FT, NT) / (FT).  Quantities are
+// rescaled in f32 to the quantity left when they sum past it; the reference prices
+// are the f32 means of the last 10 best quotes of the previous step, floored to the tick.
+DEV void exe_fixed_prices(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const i32* rec, const i32* st,
+                          i32 tid, const i32 (&act)[4], i32 wt0, i32 wt1, i32* lds_rows, int row) {
+    const i32 tick = c.tick_size, w = tc.n_actions, left = wsub(st[1], st[2]), sell = st[3];
+    i32 sum = 0;
+    for (int j = 0; j < w; ++j) sum = wadd(sum, act[j]);
+    i32 q[4];
+    const bool rescale = sum > left;
+    for (int j = 0; j < 4; ++j) q[j] = rescale ? f2i_sat(i2f(act[j]) / i2f(sum) * i2f(left)) : act[j];
+    // best_asks[-10:].mean(axis=0)[0]: f32 sum in row order, / n  (:1089-1090)
+    const int M = c.n_msgs, m0 = M > 10 ? M - 10 : 0;
+    float sa = 0.0f, sb = 0.0f;
+    for (int m = m0; m < M; ++m) {
+        sa += i2f(rec[c.off_best_asks + m * 2]);
+        sb += i2f(rec[c.off_best_bids + m * 2]);
+    }
+    const float n = (float)(M - m0), ft = (float)tick;
+    const i32 ba = f2i_sat(ffloordiv(sa / n, ft) * ft), bb = f2i_sat(ffloordiv(sb / n, ft) * ft);
+    i32 lv[4];  // FT, M, NT, PP
+    if (sell) {
+        lv[0] = wmul(ifloordiv(bb, tick), tick);
+        lv[1] = f2i_sat(ceilf(ffloordiv(i2f(wadd(bb, ba)) / 2.0f, ft)) * ft);
+        lv[2] = ba;
+        lv[3] = wadd(ba, wmul(tick, tc.n_ticks_in_book));
+    } else {
+        lv[0] = wmul(ifloordiv(ba, tick), tick);
+        lv[1] = wmul(ifloordiv(ifloordiv(wadd(bb, ba), 2), tick), tick);
+        lv[2] = bb;
+        lv[3] = wsub(bb, wmul(tick, tc.n_ticks_in_book));
+    }
+    i32 p[4];
+    if (w == 4) { p[0] = lv[0]; p[1] = lv[1]; p[2] = lv[2]; p[3] = lv[3]; }
+    else { p[0] = lv[0]; p[1] = lv[2]; p[2] = lv[3]; p[3] = 0; }
+    if (w == 4 && lv[1] == lv[2]) {  // mid == near touch: one order at the near touch
+        q[2] = wadd(q[2], q[1]);
+        q[1] = 0;
+        p[1] = -1;
+    }
+    const i32 side = wsub(1, wmul(sell, 2));
+    const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
+    for (int j = 0; j < w; ++j) put_row(lds_rows, row + j, 1, side, q[j], p[j], c.placeholder_order_id, tid, ta, tb);
+}
+
 // --------------------------------------------------------------- rewards
 // Per-row trade views with an optional override row (the fictional unwind
 // trade that add_trade — JaxOrderBookArrays.py:885-889 — places at the first
@@ -1804,7 +1859,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 //   actions    = randint(split(split(key, n_types)[t], n_agents_t)[i], 0, n_actions_t)
 //                (Speed_test.py:166-177), agent ag's in lane 32 + ag
 struct StepKeys {
-    Key k1, key_reset;
+    Key key, k1, key_reset;
     u32 shuffle_bits;  // lane l < A: random word of action row l
     i32 acts;          // lane 32 + ag: sampled action (rollout mode)
 };
@@ -1820,6 +1875,7 @@ DEV Key lane_key(Key v) { return Key{(u32)rdl((i32)v.a, 0), (u32)rdl((i32)v.b, 0
 DEV Key from_lane(Key v, int src) {  // per-lane gather v[src]
     return Key{(u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.a), (u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.b)};
 }
+template <bool MD>  // MD: the config may hold MultiDiscrete (fixed_prices) agent types
 DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* keys, const u32* master, u32* master_out) {
     const bool part = c.prng_partitionable;
     const int l = lane_id(), nTy = c.n_types, A = c.n_action_msgs;
@@ -1839,6 +1895,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     // L1: lane 0 k1, lane 1 key_reset, lane 2+t split(key, n_types)[t]
     const Key L1 = split_key(key, l < 2 ? 2 : nTy, l < 2 ? l : l - 2, part);
     StepKeys o;
+    o.key = key;
     o.k1 = Key{(u32)rdl((i32)L1.a, 0), (u32)rdl((i32)L1.b, 0)};
     o.key_reset = Key{(u32)rdl((i32)L1.a, 1), (u32)rdl((i32)L1.b, 1)};
     // L2: lane 0 sk = split(k1)[1]; agent lanes: split(sub_t, n_agents_t)[i]
@@ -1851,7 +1908,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     const Key sub = from_lane(L3a, 0);
     o.shuffle_bits = random_bits(sub, A > 0 ? A : 1, l < A ? l : 0, part);
     const u32 hb = random_bits(L3a, 1, 0, part), lb = random_bits(L3b, 1, 0, part);
-    const i32 na = agent_lane ? c.types[t].n_actions : 1;
+    const i32 na = agent_lane ? (MD ? action_hi(c.types[t]) : c.types[t].n_actions) : 1;
     const u32 span = na <= 0 ? 1u : (u32)na;  // randint(key, 0, n_actions)
     u32 mult = 65536u % span;
     mult = (mult * mult) % span;
@@ -1905,7 +1962,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
     fetch_side(fa, rec + c.off_asks, B.vs);
     fetch_side(fb, rec + c.off_bids, B.vs);
-    const StepKeys SK = step_keys(c, n_env, e, keys, master, master_out);
+    const StepKeys SK = step_keys<NFIX == 0>(c, n_env, e, keys, master, master_out);
     const Key key_reset = SK.key_reset;
     if (RC) {  // the scan's key: k1, or split(k1)[0] after the shuffle split (marl_env.py:293-294,349-351)
         B.ek = c.shuffle_action_messages ? split_key(SK.k1, 2, 0, c.prng_partitionable) : SK.k1;
@@ -1955,18 +2012,37 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     unsigned long long acc_act = 0, acc_cnl = 0, acc_flt = 0;
 #endif
     {
-        int ag = 0, arow = C, crow = 0;
+        int ag = 0, arow = C, crow = 0, aw = 0;
         const i32* st = rec + c.off_agents;
         for (int t = 0; t < c.n_types; ++t) {
             const hftlob_agent_type_cfg& tc = c.types[t];
             for (int i = 0; i < tc.n_agents; ++i, ++ag) {
                 const i32 tid = wsub(tc.trader_id0, i);
-                i32 act;
-                if (master) {  // Speed_test.py:166-177, sampled by step_keys
-                    act = rdl(SK.acts, 32 + ag);
-                    if (actions_io && l == 0) actions_io[(size_t)e * c.n_agents + ag] = act;
-                } else {
-                    act = actions_io[(size_t)e * c.n_agents + ag];
+                const int w = tc.action_width;
+                i32* aio = actions_io ? actions_io + (size_t)e * c.action_words + aw : nullptr;
+                aw += w;
+                i32 act, av[4] = {0, 0, 0, 0};
+                if (NFIX > 0 || w == 1) {  // the 100/100 kernel is launched for Discrete spaces only
+                    if (master) {  // Speed_test.py:166-177, sampled by step_keys
+                        act = rdl(SK.acts, 32 + ag);
+                        if (aio && l == 0) aio[0] = act;
+                    } else {
+                        act = aio[0];
+                    }
+                    av[0] = act;
+                } else {  // MultiDiscrete: lane j < w draws word j (spaces.py:57-65)
+                    i32 v = 0;
+                    if (master) {
+                        const bool part = c.prng_partitionable;
+                        const Key ka = split_key(split_key(SK.key, c.n_types, t, part), tc.n_agents, i, part);
+                        v = randint_vec(ka, w, l < w ? l : 0, 0, action_hi(tc), part);
+                        if (aio && l < w) aio[l] = v;
+                    } else if (l < w) {
+                        v = aio[l];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) av[j] = rdl(v, j);
+                    act = av[0];
                 }
                 i32 s4[4] = {st[0], st[1], st[2], st[3]};
                 ActX x{0, 0, 0, 0, 0, 0};
@@ -1986,7 +2062,10 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                     cancel_rows(B.a, R, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
                     STAMP_ACC(acc_cnl, ta1);
                 } else {
-                    exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, max_steps, rows, arow);
+                    if (NFIX == 0 && tc.action_space == HFTLOB_EXE_ACT_FIXED_PRICES)
+                        exe_fixed_prices(c, tc, rec, s4, tid, av, wt0, wt1, rows, arow);
+                    else
+                        exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, max_steps, rows, arow);
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
                     const i32 sell = s4[3];
@@ -2004,6 +2083,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
                 }
                 if (tc.n_action_msgs == 2) filter_rows<2>(rows, arow, crow, B.a.scr);
                 else if (tc.n_action_msgs == 4) filter_rows<4>(rows, arow, crow, B.a.scr);
+                else if (NFIX == 0 && tc.n_action_msgs == 3) filter_rows<3>(rows, arow, crow, B.a.scr);  // fixed_prices
                 else filter_rows<1>(rows, arow, crow, B.a.scr);
                 STAMP_ACC(acc_flt, ta2);
                 arow += tc.n_action_msgs;
@@ -2236,12 +2316,17 @@ __global__ void k_sample_actions(hftlob_env_cfg c, int n_env, const u32* __restr
     if (e >= n_env) return;
     const bool part = c.prng_partitionable;
     const Key k{keys[2 * e], keys[2 * e + 1]};
-    int a = 0;
+    i32* out = actions + (size_t)e * c.action_words;
     for (int t = 0; t < c.n_types; ++t) {
+        const hftlob_agent_type_cfg& tc = c.types[t];
         const Key sub = split_key(k, c.n_types, t, part);
-        for (int i = 0; i < c.types[t].n_agents; ++i, ++a)
-            actions[(size_t)e * c.n_agents + a] =
-                randint(split_key(sub, c.types[t].n_agents, i, part), 0, c.types[t].n_actions, part);
+        const int w = tc.action_width;
+        // Discrete(n_actions) or MultiDiscrete([fixed_quant_value] * w) (spaces.py:57-65)
+        const i32 hi = action_hi(tc);
+        for (int i = 0; i < tc.n_agents; ++i) {
+            const Key ka = split_key(sub, tc.n_agents, i, part);
+            for (int j = 0; j < w; ++j) *out++ = randint_vec(ka, w, j, 0, hi, part);
+        }
     }
 }
 __global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__ keys, u32* __restrict__ out) {
@@ -2310,6 +2395,11 @@ int hftlob_book_process(const hftlob_lob_cfg* cfg, int n_env, int n_msg, const u
     return launch_status();
 }
 
+static bool has_fixed_prices(const hftlob_env_cfg* c) {
+    for (int t = 0; t < c->n_types; ++t)
+        if (c->types[t].kind == HFTLOB_AGENT_EXE && c->types[t].action_space == HFTLOB_EXE_ACT_FIXED_PRICES) return true;
+    return false;
+}
 static int check_env(const hftlob_env_cfg* c) {
     if (!c) return fail(HFTLOB_ENULL, "null cfg");
     int rc = check_lob(&c->lob);
@@ -2336,10 +2426,17 @@ static int check_env(const hftlob_env_cfg* c) {
                 tc.bob_v0 <= 0)
                 return fail(HFTLOB_EINVAL, "bob_v0 must be positive");
             if (tc.n_action_msgs != 2 || tc.n_msgs != 4) return fail(HFTLOB_EINVAL, "MM message counts");
+            if (tc.action_width != 1) return fail(HFTLOB_EINVAL, "MM action_width must be 1");
         } else if (tc.kind == HFTLOB_AGENT_EXE) {
             const int a = tc.action_space;
-            const int na = a == HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX ? 4 : (a == HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG ? 1 : 2);
-            if (a < 0 || a > HFTLOB_EXE_ACT_TWAP) return fail(HFTLOB_EINVAL, "EXE action_space");
+            const int na = a == HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX ? 4
+                         : a == HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG    ? 1
+                         : a == HFTLOB_EXE_ACT_FIXED_PRICES         ? tc.n_actions : 2;
+            if (a < 0 || a > HFTLOB_EXE_ACT_FIXED_PRICES) return fail(HFTLOB_EINVAL, "EXE action_space");
+            if (a == HFTLOB_EXE_ACT_FIXED_PRICES && (tc.n_actions < 1 || tc.n_actions > 4))
+                return fail(HFTLOB_EINVAL, "fixed_prices: n_actions must be 1..4 (exec_env.py:1042-1073)");
+            if (tc.action_width != (a == HFTLOB_EXE_ACT_FIXED_PRICES ? tc.n_actions : 1))
+                return fail(HFTLOB_EINVAL, "EXE action_width");
             if (tc.n_action_msgs != na || tc.n_msgs != 2 * na) return fail(HFTLOB_EINVAL, "EXE message counts");
             if (a == HFTLOB_EXE_ACT_TWAP && c->ep_type != 0) return fail(HFTLOB_EINVAL, "twap needs fixed_steps");
             if (tc.observation_space < 0 || tc.observation_space > HFTLOB_EXE_OBS_SIMPLEST_CASE)
@@ -2347,6 +2444,9 @@ static int check_env(const hftlob_env_cfg* c) {
         } else return fail(HFTLOB_EINVAL, "unknown agent kind");
     }
     if (agents != c->n_agents) return fail(HFTLOB_EINVAL, "n_agents mismatch");
+    int words = 0;
+    for (int t = 0; t < c->n_types; ++t) words += c->types[t].n_agents * c->types[t].action_width;
+    if (words != c->action_words) return fail(HFTLOB_EINVAL, "action_words mismatch");
     return HFTLOB_OK;
 }
 
@@ -2384,7 +2484,9 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, const uint32_t*
         if (S == 1) LAUNCH_STEP(1, 0, true);
         else if (S == 2) LAUNCH_STEP(2, 0, true);
         else LAUNCH_STEP(4, 0, true);
-    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0) LAUNCH_STEP(2, 100, false);
+    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0 &&
+               !has_fixed_prices(cfg))  // the 100/100 kernel has no MultiDiscrete / fixed_prices path
+        LAUNCH_STEP(2, 100, false);
     else if (S == 1) LAUNCH_STEP(1, 0, false);
     else if (S == 2) LAUNCH_STEP(2, 0, false);
     else LAUNCH_STEP(4, 0, false);

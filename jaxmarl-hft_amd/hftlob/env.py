@@ -26,11 +26,11 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import MarketMaking_EnvironmentConfig, MultiAgentConfig
+from .config import Execution_EnvironmentConfig, MarketMaking_EnvironmentConfig, MultiAgentConfig
 from .data.synthetic import LobsterDay, generate_day
 from .data.windows import Windows, init_messages, loaded_rows, make_windows
 from .engine import book_process_
-from .layout import (AGENT_MM, EXE_FLOAT, EXE_WORDS, INFO_AGENT_WORDS, INFO_EXE, INFO_MM, INFO_WORLD,
+from .layout import (AGENT_MM, EXE_FLOAT, action_width, EXE_WORDS, INFO_AGENT_WORDS, INFO_EXE, INFO_MM, INFO_WORLD,
                      INFO_WORLD_WORDS, MM_FLOAT, MM_WORDS, EnvLayout, StepOut, pack_env_cfg, trader_ids)
 
 
@@ -38,6 +38,13 @@ from .layout import (AGENT_MM, EXE_FLOAT, EXE_WORDS, INFO_AGENT_WORDS, INFO_EXE,
 class Discrete:
     def __init__(self, n: int):
         self.n, self.shape, self.dtype = int(n), (), torch.int32
+
+
+class MultiDiscrete:
+    """from_JAXMARL/spaces.py:45-70: one categorical per dimension."""
+    def __init__(self, num_categories):
+        self.n = [int(x) for x in num_categories]
+        self.shape, self.dtype = (len(self.n),), torch.int32
 
 
 class Box:
@@ -171,7 +178,12 @@ class MARLEnv:
         L = self.layout
         self.num_msgs_per_step = L.n_msgs
         self.num_action_msgs_per_step_by_all_agents = L.n_action_msgs
-        self.action_spaces = [Discrete(a.n_actions) for a in self.list_of_agents_configs]
+        # exec_env.py:2164-2183 / mm_env.py action_space(): Discrete, or MultiDiscrete for EXE fixed_prices
+        self.action_widths = [action_width(a) for a in self.list_of_agents_configs]
+        self.action_spaces = [MultiDiscrete([a.fixed_quant_value] * a.n_actions)
+                              if isinstance(a, Execution_EnvironmentConfig) and a.action_space == "fixed_prices"
+                              else Discrete(a.n_actions) for a in self.list_of_agents_configs]
+        self.action_words = int(self.cfg_c.action_words)   # int32 words per env of the actions buffer
         self.observation_spaces = [Box(-1000 if isinstance(a, MarketMaking_EnvironmentConfig) else -10000,
                                        1000 if isinstance(a, MarketMaking_EnvironmentConfig) else 10000,
                                        (d,)) for a, d in zip(self.list_of_agents_configs, L.obs_dims)]
@@ -256,15 +268,26 @@ class MARLEnv:
         return key.to(self.device).contiguous()
 
     def _actions(self, actions, E: int) -> torch.Tensor:
+        """Per-type actions ([E, n_t] Discrete, [E, n_t, width] MultiDiscrete) or one
+        [E, action_words] tensor -> the flat int32 actions buffer of the C ABI."""
         if isinstance(actions, torch.Tensor):
             a = actions
         else:
             cols = []
-            for x, n in zip(actions, self.multi_agent_config.number_of_agents_per_type):
+            for x, n, wd in zip(actions, self.multi_agent_config.number_of_agents_per_type, self.action_widths):
                 x = torch.as_tensor(x, device=self.device)
-                cols.append(x.reshape(E, n))
+                cols.append(x.reshape(E, n * wd))
             a = torch.cat(cols, dim=1)
-        return a.to(device=self.device, dtype=torch.int32).reshape(E, self.num_agents).contiguous()
+        return a.to(device=self.device, dtype=torch.int32).reshape(E, self.action_words).contiguous()
+
+    def split_actions(self, flat: torch.Tensor):
+        """[E, action_words] -> per-type list ([E, n_t] or [E, n_t, width]), the inverse of _actions."""
+        out, k = [], 0
+        for n, wd in zip(self.multi_agent_config.number_of_agents_per_type, self.action_widths):
+            x = flat[:, k:k + n * wd]
+            out.append(x if isinstance(self.action_spaces[len(out)], Discrete) else x.reshape(-1, n, wd))
+            k += n * wd
+        return out
 
     def _info(self, o, E):
         if o["info"] is None:
@@ -325,13 +348,13 @@ class MARLEnv:
                      params: MultiAgentParams, actions_out: Optional[torch.Tensor] = None):
         """One Speed_test rollout step (Speed_test.py:165-185) in one launch:
         ``key_out, *step_keys = split(key_in, E + 1)``, per-type randint actions
-        from the step keys (written to ``actions_out`` [E, num_agents] if given),
+        from the step keys (written to ``actions_out`` [E, action_words] if given),
         then ``step``.  key_in / key_out: distinct uint32 [2] device tensors."""
         E = state.buf.shape[0]
         o = self._outputs(E)
-        if actions_out is not None and (tuple(actions_out.shape) != (E, self.num_agents)
+        if actions_out is not None and (tuple(actions_out.shape) != (E, self.action_words)
                                         or actions_out.dtype != torch.int32):
-            raise ValueError("actions_out must be int32 [E, num_agents]")
+            raise ValueError("actions_out must be int32 [E, action_words]")
         _lib.check(_lib.lib().hftlob_env_step_sampled(
             C.byref(self.cfg_c), E, _lib.ptr(key_in), _lib.ptr(key_out), _lib.ptr(actions_out),
             _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
@@ -346,9 +369,10 @@ class MARLEnv:
         return obs, state, rewards, dones, self._info(o, E)
 
     def sample_actions(self, key: torch.Tensor) -> torch.Tensor:
-        """Speed_test.py:166-177 random actions on device: int32 [E, num_agents]."""
+        """Speed_test.py:166-177 random actions on device: int32 [E, action_words]
+        (== [E, num_agents] unless an agent type has a MultiDiscrete space)."""
         keys = self._keys(key)
-        acts = torch.empty((keys.shape[0], self.num_agents), dtype=torch.int32, device=self.device)
+        acts = torch.empty((keys.shape[0], self.action_words), dtype=torch.int32, device=self.device)
         _lib.check(_lib.lib().hftlob_sample_actions(C.byref(self.cfg_c), keys.shape[0], _lib.ptr(keys),
                                                     _lib.ptr(acts), _lib.stream_ptr()))
         return acts

@@ -54,7 +54,7 @@ class AgentTypeCfg(C.Structure):
         ("bob_v0", C.c_int32), ("n_ticks_offset", C.c_int32), ("simple_nothing_action", C.c_int32),
         ("multiplier_type", C.c_int32), ("spread_multiplier", C.c_float), ("skew_multiplier", C.c_float),
         ("avst_var", C.c_float), ("avst_k", C.c_float), ("avst_log_term", C.c_float * 8),
-        ("doom_penalty_is_float", C.c_int32), ("doom_penalty_f32", C.c_float)]
+        ("doom_penalty_is_float", C.c_int32), ("doom_penalty_f32", C.c_float), ("action_width", C.c_int32)]
 
 
 class EnvCfg(C.Structure):
@@ -65,7 +65,7 @@ class EnvCfg(C.Structure):
         "shuffle_action_messages", "prng_partitionable", "n_types", "n_agents", "obs_stride",
         "rec_words", "init_rec_words", "off_asks", "off_bids", "off_trades", "off_loaded",
         "off_best_bids", "off_best_asks", "off_world", "off_agents", "info_words")] + [
-        ("_pad", C.c_int32 * 2), ("types", AgentTypeCfg * MAX_TYPES)]
+        ("action_words", C.c_int32), ("_pad", C.c_int32 * 1), ("types", AgentTypeCfg * MAX_TYPES)]
 
 
 class StepOut(C.Structure):
@@ -83,7 +83,7 @@ MM_REWARD = {"portfolio_value": 0, "buy_sell_pnl": 1, "complex": 2, "zero_inv": 
              "spooner_scaled": 8, "delta_portfolio_value": 9}
 PRICE = {"mid": 0, "mid_avg": 1, "far_touch": 2, "near_touch": 3}
 INV_PEN = {"none": 0, "linear": 1, "quadratic": 2, "threshold": 3}
-EXE_ACTION = {"fixed_quants_complex": 0, "simplest_case": 1, "fixed_quants_1msg": 2, "twap": 3}
+EXE_ACTION = {"fixed_quants_complex": 0, "simplest_case": 1, "fixed_quants_1msg": 2, "twap": 3, "fixed_prices": 4}
 EXE_OBS = {"engineered": 0, "basic": 1, "simplest_case": 2}
 EXE_REWARD = {"normal": 0, "finish_fast": 1}
 TASK = {"random": 0, "buy": 1, "sell": 2}
@@ -196,6 +196,14 @@ def _f(x) -> float:
     return float(x)
 
 
+def action_width(agent_cfg) -> int:
+    """int32 words of one agent's action: n_actions for the EXE fixed_prices
+    MultiDiscrete space (exec_env.py:2167-2171), 1 for every Discrete space."""
+    if isinstance(agent_cfg, Execution_EnvironmentConfig) and agent_cfg.action_space == "fixed_prices":
+        return int(agent_cfg.n_actions)
+    return 1
+
+
 def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
     a = AgentTypeCfg()
     a.n_agents, a.trader_id0 = n_agents, trader_id0
@@ -203,6 +211,7 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
     a.obs_dim = obs_dim(t, world)
     a.normalize, a.time_delay_obs_act, a.fixed_quant_value = int(t.normalize), t.time_delay_obs_act, t.fixed_quant_value
     a.reward_scaling_quo = _f(t.reward_scaling_quo)
+    a.action_width = action_width(t)
     if isinstance(t, MarketMaking_EnvironmentConfig):
         a.kind = AGENT_MM
         if t.action_space == "fixed_prices":
@@ -253,9 +262,9 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
             raise NotImplementedError("EXE action_space 'fixed_quants': the reference's _getActionMsgs_fixedQuant "
                                       "returns a bare array that get_messages unpacks into two values "
                                       "(exec_env.py:727,1239-1244)")
-        if t.action_space == "fixed_prices":
-            raise NotImplementedError("EXE action_space 'fixed_prices' takes a Box action vector per agent; the "
-                                      "batched action buffer of the C ABI is one Discrete int per agent")
+        if t.action_space == "fixed_prices" and t.n_actions not in (1, 2, 3, 4):
+            raise ValueError(f"EXE fixed_prices n_actions={t.n_actions}: the price-level functions "
+                             "return 1..4 levels (exec_env.py:1042-1076)")
         if t.action_space not in EXE_ACTION:
             raise ValueError("Invalid action_space specified.")
         if t.action_space == "fixed_quants_1msg" and t.larger_far_touch_quant:
@@ -313,6 +322,8 @@ def pack_env_cfg(cfg: MultiAgentConfig, n_windows: int, n_data_rows: int,
     c.order_id_counter_start = w.order_id_counter_start_when_resetting
     c.shuffle_action_messages, c.prng_partitionable = int(w.shuffle_action_messages), int(prng_partitionable)
     c.n_types, c.n_agents, c.obs_stride = len(cfg.dict_of_agents_configs), len(L.agent_kinds), L.obs_stride
+    c.action_words = sum(action_width(t) * n for t, n in zip(cfg.dict_of_agents_configs.values(),
+                                                             cfg.number_of_agents_per_type))
     for name in ("rec_words", "init_rec_words", "off_asks", "off_bids", "off_trades", "off_loaded",
                  "off_best_bids", "off_best_asks", "off_world", "off_agents", "info_words"):
         setattr(c, name, getattr(L, name))

@@ -164,6 +164,10 @@ class IPPOTrainer:
         self.n_actors = [n * self.E for n in self.n_agents]
         world = dist.get_world_size() if dist is not None else 1
         self.num_updates = max(1, int(c["TOTAL_TIMESTEPS"] // self.T // (self.E * world)))
+        for i, sp in enumerate(env.action_spaces):
+            if not isinstance(getattr(sp, "n", None), int):   # the categorical head is Dense(action_space.n)
+                raise NotImplementedError(f"agent type {i}: IPPO-RNN needs a Discrete action space "
+                                          "(ippo_rnn_JAXMARL.py ActorCriticRNN; EXE fixed_prices is MultiDiscrete)")
         torch.manual_seed(c["SEED"])  # the same initial parameters on every rank
         self.nets = [ActorCriticRNN(env.observation_spaces[i].shape[0], env.action_spaces[i].n, c["FC_DIM_SIZE"],
                                     c["GRU_HIDDEN_DIM"]).to(self.device) for i in range(nt)]

@@ -158,18 +158,22 @@ static u32 random_bits_i(const u32* key, int n, int i, int part) {
     return y1;
 }
 
-/* jax.random.randint(key, (), lo, hi) for int32 */
-i32 oracle_randint(const u32* key, i32 lo, i32 hi, int part) {
+/* jax.random.randint(key, (n,), lo, hi)[j] for int32 (jax/_src/random.py _randint: two
+ * random_bits draws of the shape from split(key), folded modulo the span) */
+static i32 randint_shaped(const u32* key, int n, int j, i32 lo, i32 hi, int part) {
     u32 k1[2], k2[2];
     oracle_split(key, 2, 0, part, k1);
     oracle_split(key, 2, 1, part, k2);
-    u32 hb = random_bits_i(k1, 1, 0, part), lb = random_bits_i(k2, 1, 0, part);
+    u32 hb = random_bits_i(k1, n, j, part), lb = random_bits_i(k2, n, j, part);
     u32 span = (hi <= lo) ? 1u : (u32)hi - (u32)lo;
     u32 mult = 65536u % span;
     mult = (mult * mult) % span;
     u32 off = ((hb % span) * mult + (lb % span)) % span;
     return (i32)((u32)lo + off);
 }
+
+/* jax.random.randint(key, (), lo, hi) for int32 */
+i32 oracle_randint(const u32* key, i32 lo, i32 hi, int part) { return randint_shaped(key, 1, 0, lo, hi, part); }
 
 /* jax.random.permutation(key, arange(n)): perm[j] = source row of output j */
 void oracle_permutation(const u32* key, int n, int part, int* perm) {
@@ -779,6 +783,64 @@ static void exe_fqc(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, En
     }
 }
 
+/* EXE _getActionMsgs_fixedPrice — exec_env.py:1001-1123.  `action` holds n_actions
+ * (1..4) quantities, one per price level. */
+static void exe_fixed_price(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env* E, const i32* st, i32 tid,
+                            const i32* action, i32* out) {
+    int n = tc->n_actions;
+    i32 tick = c->tick_size, left = wsub(st[1], st[2]), sell = st[3];
+    /* :1005-1010: if sum(action) > left: (action / sum(action) * left).astype(int32) (f32) */
+    i32 sum = 0, a[4];
+    for (int k = 0; k < n; ++k) sum = wadd(sum, action[k]);
+    for (int k = 0; k < n; ++k)
+        a[k] = sum > left ? f2i_sat((float)action[k] / (float)sum * (float)left) : action[k];
+    /* :1089-1090: best_asks[-10:].mean(axis=0)[0] // tick * tick, as int32 */
+    int M = c->n_msgs, lo = M > 10 ? M - 10 : 0;
+    float ma = 0.0f, mb = 0.0f;
+    for (int m = lo; m < M; ++m) { ma += (float)BASKS(E)[m * 2]; mb += (float)BBIDS(E)[m * 2]; }
+    ma /= (float)(M - lo);
+    mb /= (float)(M - lo);
+    i32 best_ask = f2i_sat(ffloordiv(ma, (float)tick) * (float)tick);
+    i32 best_bid = f2i_sat(ffloordiv(mb, (float)tick) * (float)tick);
+    /* buy_task_prices / sell_task_prices :1043-1076 -> (FT, M, NT, PP, MKT) */
+    i32 FT, Mp, NT, PP, MKT;
+    if (sell) {
+        FT = wmul(ifloordiv(best_bid, tick), tick);
+        Mp = f2i_sat(ceilf(ffloordiv((float)wadd(best_bid, best_ask) / 2.0f, (float)tick)) * (float)tick);
+        NT = best_ask;
+        PP = wadd(best_ask, wmul(tick, tc->n_ticks_in_book));
+        MKT = 0;
+    } else {
+        FT = wmul(ifloordiv(best_ask, tick), tick);
+        Mp = wmul(ifloordiv(ifloordiv(wadd(best_bid, best_ask), 2), tick), tick);
+        NT = best_bid;
+        PP = wsub(best_bid, wmul(tick, tc->n_ticks_in_book));
+        MKT = c->lob.maxint;
+    }
+    i32 levels[5];
+    int nl = 0;
+    levels[nl++] = FT;
+    if (n == 4) levels[nl++] = Mp;
+    if (n >= 2) levels[nl++] = NT;
+    if (n >= 3) levels[nl++] = PP;
+    levels[nl++] = MKT;
+    /* normal_quant_price :1013-1033: prices = price_levels[:-1]; n == 4 and M == NT: merge into NT */
+    i32 q[4], p[4];
+    for (int k = 0; k < n; ++k) { q[k] = a[k]; p[k] = levels[k]; }
+    if (n == 4 && levels[1] == levels[2]) {
+        q[2] = wadd(q[2], q[1]);
+        q[1] = 0;
+        p[1] = -1;
+    }
+    i32 side = wsub(1, wmul(sell, 2));
+    const i32* wt = WORLD(E);
+    for (int k = 0; k < n; ++k) {
+        i32* o = out + k * 8;
+        o[0] = 1; o[1] = side; o[2] = q[k]; o[3] = p[k]; o[4] = c->placeholder_order_id; o[5] = tid;
+        o[6] = wadd(wt[0], tc->time_delay_obs_act); o[7] = wadd(wt[1], tc->time_delay_obs_act);
+    }
+}
+
 /* ---- trade-log helpers for rewards */
 /* add_trade — JaxOrderBookArrays.py:885-889: first row holding ANY -1 field */
 static void add_trade(i32* tr, int nT, const i32* row) {
@@ -1246,11 +1308,16 @@ static int env_cfg_ok(const hftlob_env_cfg* c) {
     if ((c->ep_type != 0 && c->ep_type != 1) || c->n_types < 1 || c->n_types > HFTLOB_MAX_TYPES) return 0;
     if (c->n_msgs > HFTLOB_MAX_MSGS || c->n_agents > HFTLOB_MAX_AGENTS || c->n_windows < 1) return 0;
     if (c->obs_stride > HFTLOB_MAX_OBS) return 0;
+    int words = 0;
     for (int t = 0; t < c->n_types; ++t) {
         const hftlob_agent_type_cfg* tc = &c->types[t];
         if (tc->kind == HFTLOB_AGENT_MM && tc->sell_buy_all_option && tc->action_space != HFTLOB_MM_ACT_SIMPLE) return 0;
+        if (tc->kind == HFTLOB_AGENT_EXE && tc->action_space == HFTLOB_EXE_ACT_FIXED_PRICES &&
+            (tc->n_actions < 1 || tc->n_actions > 4 || tc->action_width != tc->n_actions))
+            return 0;
+        words += tc->n_agents * tc->action_width;
     }
-    return 1;
+    return words == c->action_words;
 }
 
 int oracle_env_reset(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* init_states, i32* state,
@@ -1292,6 +1359,7 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     i32 actm[HFTLOB_MAX_MSGS * 8], cnlm[HFTLOB_MAX_MSGS * 8];
     ActX ax[HFTLOB_MAX_AGENTS];
     int na = 0, nc = 0, a = 0;
+    const i32* av = act; /* agent a's action words (action_width of its type) */
     i32* st = rec + c->off_agents;
     i32* sts[HFTLOB_MAX_AGENTS];
     for (int t = 0; t < c->n_types; ++t) {
@@ -1302,15 +1370,18 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
             i32* am = actm + na * 8;
             i32* cm = cnlm + nc * 8;
             memset(&ax[a], 0, sizeof ax[a]);
+            const i32* aa = av;
+            av += tc->action_width;
             if (tc->kind == HFTLOB_AGENT_MM) {
-                if (tc->action_space == HFTLOB_MM_ACT_DIRECTIONAL) mm_directional(c, tc, &E, tid, act[a], am, &ax[a]);
-                else if (tc->action_space == HFTLOB_MM_ACT_FIXED_QUANTS) mm_fixed_quant(c, tc, &E, st, tid, act[a], am, &ax[a]);
-                else mm_other_actions(c, tc, &E, st, tid, act[a], am, &ax[a]);
+                if (tc->action_space == HFTLOB_MM_ACT_DIRECTIONAL) mm_directional(c, tc, &E, tid, aa[0], am, &ax[a]);
+                else if (tc->action_space == HFTLOB_MM_ACT_FIXED_QUANTS) mm_fixed_quant(c, tc, &E, st, tid, aa[0], am, &ax[a]);
+                else mm_other_actions(c, tc, &E, st, tid, aa[0], am, &ax[a]);
                 int sz = tc->n_msgs / 4;
                 get_cancel_msgs(BIDS(&E), nO, tid, sz, 1, W[0], W[1], cm);
                 get_cancel_msgs(ASKS(&E), nO, tid, sz, -1, W[0], W[1], cm + sz * 8);
             } else {
-                exe_fqc(c, tc, &E, st, tid, act[a], am);
+                if (tc->action_space == HFTLOB_EXE_ACT_FIXED_PRICES) exe_fixed_price(c, tc, &E, st, tid, aa, am);
+                else exe_fqc(c, tc, &E, st, tid, aa[0], am);
                 i32 sell = st[3];
                 get_cancel_msgs(sell ? ASKS(&E) : BIDS(&E), nO, tid, tc->n_msgs / 2, wsub(1, wmul(sell, 2)), W[0], W[1],
                                 cm);
@@ -1456,7 +1527,7 @@ int oracle_env_step(const hftlob_env_cfg* c, int n_env, const u32* keys, const i
     if (!env_cfg_ok(c)) return HFTLOB_EINVAL;
 #pragma omp parallel for schedule(dynamic, 16)
     for (int e = 0; e < n_env; ++e)
-        env_step_one(c, keys + 2 * e, actions + (size_t)e * c->n_agents, msg_data, init_states,
+        env_step_one(c, keys + 2 * e, actions + (size_t)e * c->action_words, msg_data, init_states,
                      state + (size_t)e * c->rec_words, obs + (size_t)e * c->n_agents * c->obs_stride,
                      rew + (size_t)e * c->n_agents, done_all + e, dones + (size_t)e * c->n_agents,
                      info ? info + (size_t)e * c->info_words : NULL);
@@ -1467,14 +1538,21 @@ int oracle_env_step(const hftlob_env_cfg* c, int n_env, const u32* keys, const i
 void oracle_sample_actions(const hftlob_env_cfg* c, int n_env, const u32* keys, i32* actions) {
     int part = c->prng_partitionable;
     for (int e = 0; e < n_env; ++e) {
-        int a = 0;
+        i32* out = actions + (size_t)e * c->action_words;
         for (int t = 0; t < c->n_types; ++t) {
+            const hftlob_agent_type_cfg* tc = &c->types[t];
             u32 sub[2];
             oracle_split(keys + 2 * e, c->n_types, t, part, sub);
-            for (int i = 0; i < c->types[t].n_agents; ++i, ++a) {
+            for (int i = 0; i < tc->n_agents; ++i) {
                 u32 ki[2];
-                oracle_split(sub, c->types[t].n_agents, i, part, ki);
-                actions[(size_t)e * c->n_agents + a] = oracle_randint(ki, 0, c->types[t].n_actions, part);
+                oracle_split(sub, tc->n_agents, i, part, ki);
+                if (tc->kind == HFTLOB_AGENT_EXE && tc->action_space == HFTLOB_EXE_ACT_FIXED_PRICES) {
+                    /* MultiDiscrete([fixed_quant_value] * n_actions).sample (spaces.py:57-65) */
+                    for (int j = 0; j < tc->n_actions; ++j)
+                        *out++ = randint_shaped(ki, tc->n_actions, j, 0, tc->fixed_quant_value, part);
+                } else {
+                    *out++ = oracle_randint(ki, 0, tc->n_actions, part); /* Discrete.sample */
+                }
             }
         }
     }
@@ -1489,15 +1567,20 @@ void oracle_split_keys(int n_env, int n, int part, const u32* keys, u32* out) {
  * record `rec`: the agent-level checker of the action spaces (tests only).
  * out: 2 rows of 8; extras: bid_price, ask_price, bid_dist, ask_dist, bid_quant,
  * ask_quant, empty_book. */
-int oracle_mm_action_msgs(const hftlob_env_cfg* c, int type, int agent, const i32* rec, i32 action, i32* out,
-                          i32* extras) {
+int oracle_mm_action_msgs(const hftlob_env_cfg* c, int type, int agent, const i32* rec, const i32* action_words,
+                          i32* out, i32* extras) {
+    i32 action = action_words[0];
     if (type < 0 || type >= c->n_types) return HFTLOB_EINVAL;
     if (c->types[type].kind == HFTLOB_AGENT_EXE) { /* EXE: up to 4 rows, no extras */
         const hftlob_agent_type_cfg* te = &c->types[type];
         int off = c->off_agents;
         for (int t = 0; t < type; ++t) off += c->types[t].n_agents * agent_words(&c->types[t]);
         Env E = {c, (i32*)rec};
-        exe_fqc(c, te, &E, rec + off + agent * agent_words(te), wsub(te->trader_id0, agent), action, out);
+        const i32* st = rec + off + agent * agent_words(te);
+        if (te->action_space == HFTLOB_EXE_ACT_FIXED_PRICES)
+            exe_fixed_price(c, te, &E, st, wsub(te->trader_id0, agent), action_words, out);
+        else
+            exe_fqc(c, te, &E, st, wsub(te->trader_id0, agent), action, out);
         memset(extras, 0, 7 * sizeof(i32));
         return HFTLOB_OK;
     }

@@ -33,7 +33,7 @@ def lib():
         L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
         L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
-        L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int32, vp, vp]
+        L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp]
         L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
         L.oracle_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)] * 2
         L.oracle_randint.argtypes = [vp, C.c_int32, C.c_int32, C.c_int]
@@ -108,7 +108,7 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
     """Returns (state', obs, rewards, done_all, dones, info); `state` is not modified."""
     keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
     E = keys.shape[0]
-    actions = np.ascontiguousarray(actions, dtype=np.int32).reshape(E, env_cfg.n_agents)
+    actions = np.ascontiguousarray(actions, dtype=np.int32).reshape(E, env_cfg.action_words)
     st = np.array(state, dtype=np.int32, copy=True, order="C")
     obs = np.zeros((E, env_cfg.n_agents, env_cfg.obs_stride), dtype=np.float32)
     rew = np.zeros((E, env_cfg.n_agents), dtype=np.float32)
@@ -123,17 +123,21 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
 
 def mm_action_msgs(env_cfg, type_idx, agent, rec, action):
     """(rows int32 [n_action_msgs, 8], extras [7]) of one agent's raw action messages for record `rec`
-    (MM: 2 rows + extras; EXE: n_action_msgs rows)."""
+    (MM: 2 rows + extras; EXE: n_action_msgs rows).  `action`: an int, or the action_width
+    quantities of an EXE fixed_prices agent."""
     out = np.zeros((4, 8), np.int32)
     ex = np.zeros(7, np.int32)
     rec = np.ascontiguousarray(rec, dtype=np.int32)
-    _chk(lib().oracle_mm_action_msgs(C.byref(env_cfg), type_idx, agent, _p(rec), int(action), _p(out), _p(ex)))
+    aw = np.zeros(4, np.int32)
+    a = np.atleast_1d(np.asarray(action, dtype=np.int64)).astype(np.int32)
+    aw[:a.size] = a
+    _chk(lib().oracle_mm_action_msgs(C.byref(env_cfg), type_idx, agent, _p(rec), _p(aw), _p(out), _p(ex)))
     return out[:env_cfg.types[type_idx].n_action_msgs], ex
 
 
 def sample_actions(env_cfg, keys):
     keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
-    out = np.zeros((keys.shape[0], env_cfg.n_agents), dtype=np.int32)
+    out = np.zeros((keys.shape[0], env_cfg.action_words), dtype=np.int32)
     lib().oracle_sample_actions(C.byref(env_cfg), keys.shape[0], _p(keys), _p(out))
     return out
 

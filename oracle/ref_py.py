@@ -216,3 +216,23 @@ def randint(key, lo, hi, partitionable=True):
     span = 1 if hi <= lo else (hi - lo) & 0xFFFFFFFF
     mult = (65536 % span) ** 2 % span
     return lo + (((hb % span) * mult + (lb % span)) & 0xFFFFFFFF) % span
+
+
+def random_bits(key, n, partitionable=True):
+    """jax random_bits(key, 32, (n,)): partitionable counters (0, i) -> y0 ^ y1; legacy: the iota
+    split into halves (zero-padded to even length), outputs concatenated [y0..., y1...][:n]."""
+    if partitionable:
+        return [a ^ b for a, b in (threefry2x32(key[0], key[1], 0, i) for i in range(n))]
+    half = (n + 1) // 2
+    ctr = list(range(n)) + [0] * (2 * half - n)
+    y0, y1 = zip(*[threefry2x32(key[0], key[1], ctr[i], ctr[half + i]) for i in range(half)])
+    return (list(y0) + list(y1))[:n]
+
+
+def randint_vec(key, n, lo, hi, partitionable=True):
+    """jax.random.randint(key, (n,), lo, hi) (jax/_src/random.py _randint) for int32."""
+    k1, k2 = split(key, 2, partitionable)
+    hb, lb = random_bits(k1, n, partitionable), random_bits(k2, n, partitionable)
+    span = 1 if hi <= lo else (hi - lo) & 0xFFFFFFFF
+    mult = (65536 % span) ** 2 % span
+    return [lo + (((h % span) * mult + (l % span)) & 0xFFFFFFFF) % span for h, l in zip(hb, lb)]

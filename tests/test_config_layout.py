@@ -68,7 +68,7 @@ def test_roundtrip(tmp_path, fmt):
     ("MarketMaking", dict(reward_function="bogus"), ValueError),
     ("MarketMaking", dict(unwind_price="near_touch"), ValueError),
     ("Execution", dict(action_space="fixed_quants"), NotImplementedError),   # reference unpack error
-    ("Execution", dict(action_space="fixed_prices"), NotImplementedError),   # Box actions
+    ("Execution", dict(action_space="fixed_prices", n_actions=5), ValueError),   # 1..4 price levels only
     ("Execution", dict(action_space="fixed_quants_1msg", larger_far_touch_quant=True), NotImplementedError),
     ("Execution", dict(reference_price="near_touch"), ValueError),
 ])
@@ -92,19 +92,14 @@ def test_cancel_mode_values():
 
 
 REF_CFG_DIR = "/root/reference/config/env_configs"
-GAP_CONFIGS = {"exec_debug_fixed_price.json", "exec_longrun_fixed_price.json"}
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_CFG_DIR), reason="reference configs not mounted")
 @pytest.mark.parametrize("fname", sorted(os.listdir(REF_CFG_DIR)) if os.path.isdir(REF_CFG_DIR) else [])
 def test_reference_env_configs_pack(fname):
-    """Every env config the reference ships loads with our loader; those on the HIP path pack."""
+    """Every env config the reference ships loads with our loader and packs for the HIP path."""
     from hftlob.config_io import load_config_from_file
     cfg = load_config_from_file(os.path.join(REF_CFG_DIR, fname))
-    try:
-        c, L = pack_env_cfg(cfg, 4, 100_000, True)
-    except NotImplementedError as e:       # documented gap: EXE fixed_prices (Box actions)
-        assert fname in GAP_CONFIGS and "fixed_prices" in str(e), (fname, str(e))
-        return
-    assert fname not in GAP_CONFIGS
+    c, L = pack_env_cfg(cfg, 4, 100_000, True)
     assert c.n_msgs == L.n_msgs and c.n_types == len(cfg.dict_of_agents_configs)
+    assert c.action_words == sum(c.types[t].n_agents * c.types[t].action_width for t in range(c.n_types))

@@ -135,3 +135,97 @@ def test_exe_obs_vs_numpy(obs, norm):
             assert np.array_equal(np.array(got, np.float32), np.array(want, np.float32)), (k, e, got, want)
         acts = O.sample_actions(c, keys + 3 * k)
         st, o = O.env_step(c, keys + 3 * k, acts, day.msgs, init, st)[:2]
+
+
+# ------------------------------------------------ fixed_prices (MultiDiscrete quantities)
+def _mean_last10(x):
+    """best_asks[-10:].mean(axis=0)[0] with f32 accumulation in row order."""
+    x = [int(v) for v in x[-10:]]
+    s = F(0)
+    for v in x:
+        s = F(s + F(v))
+    return F(s / F(len(x)))
+
+
+def expected_fixed_price_rows(t, w, rec, L, a_off, action):
+    """exec_env.py:1001-1123 restated in numpy."""
+    M, tick, n = L.n_msgs, w.tick_size, t.n_actions
+    st = rec[a_off:a_off + 13]
+    left, sell = int(st[1]) - int(st[2]), int(st[3])
+    a = np.atleast_1d(np.asarray(action, np.int32))
+    if int(a.sum()) > left:
+        a = (a.astype(F) / F(a.sum()) * F(left)).astype(np.int32)
+    asks = rec[L.off_best_asks:L.off_best_asks + 2 * M].reshape(M, 2)[:, 0]
+    bids = rec[L.off_best_bids:L.off_best_bids + 2 * M].reshape(M, 2)[:, 0]
+    ba = int(F(_mean_last10(asks) // F(tick)) * F(tick))
+    bb = int(F(_mean_last10(bids) // F(tick)) * F(tick))
+    if sell:
+        lv = dict(FT=bb // tick * tick, M=int(np.ceil(F(F(bb + ba) / F(2)) // F(tick)) * F(tick)), NT=ba,
+                  PP=ba + tick * t.n_ticks_in_book)
+    else:
+        lv = dict(FT=ba // tick * tick, M=(bb + ba) // 2 // tick * tick, NT=bb, PP=bb - tick * t.n_ticks_in_book)
+    names = {4: ("FT", "M", "NT", "PP"), 3: ("FT", "NT", "PP"), 2: ("FT", "NT"), 1: ("FT",)}[n]
+    prices = [lv[k] for k in names]
+    q = [int(v) for v in a]
+    if n == 4 and prices[1] == prices[2]:
+        q[2], q[1], prices[1] = q[2] + q[1], 0, -1
+    return list(zip(q, prices))
+
+
+FP_CASES = [dict(n_actions=4), dict(n_actions=4, task_size=30), dict(n_actions=3, task="sell"),
+            dict(n_actions=2, task="buy", task_size=12), dict(n_actions=1), dict(n_actions=1, task_size=5)]
+
+
+@pytest.mark.parametrize("changes", FP_CASES, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+def test_exe_fixed_price_messages_vs_numpy(changes):
+    cfg, w, day, c, L, init = _setup(dict(action_space="fixed_prices", fixed_quant_value=11, **changes))
+    t = cfg.dict_of_agents_configs["Execution"]
+    n = t.n_actions
+    assert c.types[1].action_width == n and c.action_words == 1 + n
+    E = 10
+    keys = np.arange(2 * E, dtype=np.uint32).reshape(E, 2) + 7
+    st, _ = O.env_reset(c, keys, init)
+    a_off = L.agent_offsets[1]
+    rng = np.random.default_rng(3)
+    cand = [np.zeros(n, np.int32), np.full(n, 10, np.int32), np.arange(n, dtype=np.int32) * 3,
+            np.full(n, -4, np.int32)] + [rng.integers(0, 11, n).astype(np.int32) for _ in range(6)]
+    merged = rescaled = 0
+    for k in range(8):
+        for e in range(E):
+            for act in cand:
+                rows, _ = O.mm_action_msgs(c, 1, 0, st[e], act)
+                want = expected_fixed_price_rows(t, w, st[e], L, a_off, act)
+                got = [(int(r[2]), int(r[3])) for r in rows]
+                assert got == want, f"step {k} env {e} action {act}: oracle {got} numpy {want}"
+                merged += n == 4 and want[1][1] == -1
+                left = int(st[e, a_off + 1]) - int(st[e, a_off + 2])
+                rescaled += int(act.sum()) > left
+        acts = O.sample_actions(c, keys + 5 * k)
+        assert acts.shape == (E, 1 + n) and ((acts[:, 1:] >= 0) & (acts[:, 1:] < 11)).all()
+        st = O.env_step(c, keys + 5 * k, acts, day.msgs, init, st)[0]
+    assert ("task_size" not in changes or rescaled > 0) and (n != 4 or merged > 0)   # both branches ran
+
+
+def test_mean_last10_order_free_at_tick_prices():
+    """The f32 mean of 10 tick-multiple prices below 2**26 is exact in any summation order (the
+    reference's XLA reduction order is unspecified; the restatements sum in row order)."""
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        x = rng.integers(1_000_000 // 100, 6_000_000 // 100, 10) * 100
+        assert _mean_last10(x) == F(np.sum(x.astype(F)) / F(10)) == F(np.float64(x.sum()) / 10)
+
+
+@pytest.mark.parametrize("part", [True, False])
+def test_multidiscrete_sampling_vs_numpy(part):
+    """Speed_test.py:166-177 with MultiDiscrete.sample (spaces.py:57-65): randint of shape (n,)."""
+    from oracle import ref_py as R
+    cfg = variant(builtin_config("2_player_fq_fqc"), "Execution", action_space="fixed_prices", n_actions=3,
+                  fixed_quant_value=7)
+    c, _ = pack_env_cfg(cfg, 4, 10_000, part)
+    keys = np.arange(16, dtype=np.uint32).reshape(8, 2) * 977
+    acts = O.sample_actions(c, keys)
+    for e in range(8):
+        sub = R.split(tuple(int(v) for v in keys[e]), 2, part)
+        mm = R.randint(R.split(sub[0], 1, part)[0], 0, c.types[0].n_actions, part)
+        exe = R.randint_vec(R.split(sub[1], 1, part)[0], 3, 0, 7, part)
+        assert acts[e].tolist() == [mm] + exe

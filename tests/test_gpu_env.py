@@ -220,7 +220,13 @@ EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid",
                 dict(action_space="fixed_quants_1msg"), dict(action_space="fixed_quants_1msg", task_size=40),
                 dict(action_space="twap"), dict(action_space="twap", task_size=7, task="buy"),
                 dict(observation_space="basic"), dict(observation_space="basic", normalize=False),
-                dict(observation_space="simplest_case"), dict(observation_space="simplest_case", normalize=False)]
+                dict(observation_space="simplest_case"), dict(observation_space="simplest_case", normalize=False),
+                # fixed_prices: MultiDiscrete([fixed_quant_value] * n_actions) quantities per price level
+                dict(action_space="fixed_prices", n_actions=4, fixed_quant_value=11),
+                dict(action_space="fixed_prices", n_actions=4, fixed_quant_value=11, task_size=30, task="sell"),
+                dict(action_space="fixed_prices", n_actions=3, fixed_quant_value=11, task="buy"),
+                dict(action_space="fixed_prices", n_actions=2, fixed_quant_value=11, task_size=12),
+                dict(action_space="fixed_prices", n_actions=1, fixed_quant_value=10)]
 
 
 @pytest.mark.parametrize("changes", EXE_VARIANTS, ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
@@ -228,11 +234,15 @@ def test_exe_option_parity(changes):
     rollout_parity(variant(builtin_config("2_player_fq_fqc"), "Execution", **changes), E=32, K=66)
 
 
-@pytest.mark.parametrize("name,part", [("2_player_fq_fqc", True), ("3_player_fq_fqc_dir", True),
-                                       ("2_player_fq_fqc", False)])
-def test_step_sampled_equals_split_sample_step(name, part):
-    """hftlob_env_step_sampled (one launch) == split_keys + sample_actions + env_step."""
+@pytest.mark.parametrize("name,part,exe", [("2_player_fq_fqc", True, None), ("3_player_fq_fqc_dir", True, None),
+                                           ("2_player_fq_fqc", False, None), ("2_player_fq_fqc", True, 3),
+                                           ("exec_debug_fixed_quants_complex", False, 2)])
+def test_step_sampled_equals_split_sample_step(name, part, exe):
+    """hftlob_env_step_sampled (one launch) == split_keys + sample_actions + env_step
+    (exe = n: the Execution type uses fixed_prices with n MultiDiscrete quantities)."""
     cfg = builtin_config(name)
+    if exe:
+        cfg = variant(cfg, "Execution", action_space="fixed_prices", n_actions=exe, fixed_quant_value=11)
     w = cfg.world_config
     env = MARLEnv(None, cfg, data=_day(w, 2_000_000), prng_partitionable=part)
     params = env.default_params
@@ -242,7 +252,7 @@ def test_step_sampled_equals_split_sample_step(name, part):
     s2 = s1.clone(env)
     kbuf = [torch.tensor([0, 7], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
     rng = kbuf[0].clone().reshape(1, 2)
-    acts_out = torch.empty((E, env.num_agents), dtype=torch.int32, device="cuda")
+    acts_out = torch.empty((E, env.action_words), dtype=torch.int32, device="cuda")
     for k in range(70):
         o1, s1, r1, d1, _ = env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], s1, params, acts_out)
         o1 = [x.clone() for x in o1]
