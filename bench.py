@@ -81,6 +81,9 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per captured HIP graph in the timed region (even; 0 = eager launches)")
     ap.add_argument("--config", default=CONFIG, help="builtin env config (the metric: 2_player_fq_fqc)")
+    ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
+                    help="rollout: one fused launch per step (key split + action sampling + step); "
+                         "step: split_keys, sample_actions and env.step as three launches (SURVEY.md 8(d))")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
@@ -118,15 +121,22 @@ def main():
     kbuf = [torch.tensor([0, 1 + rank], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
     nstep = [0]
 
+    rng = [kbuf[0].reshape(1, 2).clone()]
+
     def one_step():
         k = nstep[0]
-        env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)
+        if args.mode == "rollout":
+            env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)
+        else:  # Speed_test's three calls, each its own launch: split, Discrete.sample, env.step
+            ks = split_keys(rng[0], E + 1)[0]
+            rng[0], sk = ks[0:1], ks[1:]
+            env.step(sk, state, env.sample_actions(sk), params)
         nstep[0] = k + 1
 
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
-    G = args.graph_steps if args.graph_steps > 0 and args.graph_steps % 2 == 0 else 0
+    G = args.graph_steps if args.graph_steps > 0 and args.graph_steps % 2 == 0 and args.mode == "rollout" else 0
     graph = None
     if G:
         # G consecutive launches in one HIP graph; G is even, so the key ping-pong buffers line up
@@ -162,6 +172,7 @@ def main():
     D.barrier(R)
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps   # average k_env_step launch duration, HIP events
+    # (step mode: the three launches of one step together; rocprof splits them)
     elapsed = D.max_over_ranks(R, elapsed, device="cuda")
 
     if rank != 0:
@@ -197,10 +208,10 @@ def main():
         "dtype": "int32",
         "data": f"synthetic LOBSTER day ({args.n_msgs} msgs, PCG64 seed 20260403, mid {args.mid})",
         "config": {"workload": (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, 112 msgs/step, "
-                                f"auto-reset, Speed_test rollout semantics") if args.config == CONFIG else
+                                f"auto-reset, Speed_test semantics") if args.config == CONFIG else
                                f"{args.config}.json, {env.num_msgs_per_step} msgs/step, auto-reset, Speed_test semantics",
                    "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)",
-                   "launch": f"hipGraph of {G} steps" if G else "eager"},
+                   "launch": f"hipGraph of {G} steps" if G else "eager", "mode": args.mode},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                      "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env},

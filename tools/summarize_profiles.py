@@ -45,3 +45,16 @@ if sq:
     w = sum(sq["SQ_WAVES"]) / len(sq["SQ_WAVES"])
     print("== SQ counters per wave (k_env_step):",
           {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(sq.items()) if k != "SQ_WAVES"})
+lds = {}
+for r in rows("lds"):
+    if "k_env_step" in r["Kernel_Name"]:
+        lds.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+if lds:
+    w = sum(lds["SQ_WAVES"]) / len(lds["SQ_WAVES"])
+    print("== SQ LDS / issue counters per wave (k_env_step):",
+          {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(lds.items()) if k != "SQ_WAVES"})
+sm = os.path.join(d, "bench_stepmode.json")
+if os.path.exists(sm) and os.path.getsize(sm):
+    b = json.load(open(sm))
+    print("== step mode (split_keys + sample_actions + env.step, 3 launches):", b["value"], "env steps/s,",
+          b["ms_per_step"], "ms/step")
