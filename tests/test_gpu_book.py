@@ -70,3 +70,25 @@ def test_book_functional_api():
     a = torch.full((100, 6), -1, dtype=torch.int32).cuda()
     (na, nb, nt), (ba, bb) = scan_through_entire_array_save_bidask(cfg, None, msgs, (a, a, torch.full((100, 8), -1, dtype=torch.int32).cuda()), 10)
     assert ba.shape == (10, 2) and (a == -1).all()   # inputs untouched, last N rows returned
+
+
+def test_book_empty_and_max_sizes():
+    """n_env = 0 and n_msg = 0 are no-ops; nOrders = nTrades = 256 (HFTLOB_MAX_SLOTS) is parity-exact."""
+    cfg = JAXLOB_Configuration()
+    a = torch.full((0, 100, 6), -1, dtype=torch.int32, device="cuda")
+    t = torch.full((0, 100, 8), -1, dtype=torch.int32, device="cuda")
+    book_process_(cfg, torch.empty((0, 5, 8), dtype=torch.int32, device="cuda"), a, a.clone(), t)
+    a1 = torch.full((3, 100, 6), -1, dtype=torch.int32, device="cuda")
+    a1[:, 0] = torch.tensor([200, 5, 1, 1, 0, 0], dtype=torch.int32)
+    before = a1.clone()
+    t1 = torch.full((3, 100, 8), -1, dtype=torch.int32, device="cuda")
+    book_process_(cfg, torch.empty((3, 0, 8), dtype=torch.int32, device="cuda"), a1, a1.clone(), t1)
+    torch.cuda.synchronize()
+    assert torch.equal(a1, before) and (t1 == -1).all()
+    big = JAXLOB_Configuration(nOrders=256, nTrades=256)
+    E, M = 8, 400
+    init = init_book_messages(E, seed=4)
+    empty_a = np.full((E, 256, 6), -1, np.int32)
+    empty_t = np.full((E, 256, 8), -1, np.int32)
+    a0, b0, _, _, _ = O.book_process(pack_lob_cfg(big), init, empty_a, empty_a, empty_t, save_best=False)
+    _run(big, random_streams(E, M, seed=77), a0, b0, empty_t)

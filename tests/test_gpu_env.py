@@ -267,3 +267,26 @@ def test_step_sampled_equals_split_sample_step(name, part, exe):
         assert (s1.buf == s2.buf).all(), f"step {k}: state"
         assert all((a == b).all() for a, b in zip(o1, o2)) and all((a == b).all() for a, b in zip(r1, r2))
         assert (da1 == d2["__all__"]).all()
+
+
+@pytest.mark.parametrize("name,agents,changes", [
+    ("2_player_fq_fqc", [3, 2], None),                     # several agents of each type
+    ("3_player_fq_fqc_dir", [2, 2, 3], None),
+    ("2_player_fq_fqc", [2, 3], dict(action_space="fixed_prices", n_actions=3, fixed_quant_value=11)),
+    ("mm_debug_fixed_quant", [4], None),
+])
+def test_multi_agent_per_type_parity(name, agents, changes):
+    """number_of_agents_per_type > 1: trader ids, per-agent key splits, the action / cancel row
+    layout and the shuffle over more rows (marl_env.py:85-115,254-315)."""
+    cfg = builtin_config(name)
+    if changes:
+        cfg = variant(cfg, "Execution", **changes)
+    cfg = dataclasses.replace(cfg, number_of_agents_per_type=agents)
+    rollout_parity(cfg, E=24, K=66)
+
+
+def test_max_book_size_parity():
+    """nOrders = nTrades = HFTLOB_MAX_SLOTS (256): four slot sets per lane in the env kernel."""
+    cfg = builtin_config("2_player_fq_fqc")
+    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, nOrders=256, nTrades=256))
+    rollout_parity(cfg, E=16, K=40)
