@@ -916,16 +916,23 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
         B.part = cfg.prng_partitionable;
     }
     const i32* gm = msgs + (size_t)e * n_msg * 8;
+    int4 nx = make_int4(0, 0, 0, 0), ny = nx;  // message rows, loaded one chunk ahead
+    if (l < n_msg) {
+        nx = reinterpret_cast<const int4*>(gm + l * 8)[0];
+        ny = reinterpret_cast<const int4*>(gm + l * 8)[1];
+    }
     for (int base = 0; base < n_msg; base += 64) {
         const int row = base + l;
-        int4 x = make_int4(0, 0, 0, 0), y = x;
-        if (row < n_msg) {
-            x = reinterpret_cast<const int4*>(gm + row * 8)[0];
-            y = reinterpret_cast<const int4*>(gm + row * 8)[1];
+        int4 x = nx, y = ny;
+        nx = make_int4(0, 0, 0, 0);
+        ny = nx;
+        if (row + 64 < n_msg) {  // the next chunk's loads land while this one runs
+            nx = reinterpret_cast<const int4*>(gm + (row + 64) * 8)[0];
+            ny = reinterpret_cast<const int4*>(gm + (row + 64) * 8)[1];
         }
         decode_msgs(B.c, x, y);
         i32 ap = 0, aq = 0, bp = 0, bq = 0;
-        const int cnt = imin_(64, n_msg - base);
+        const int cnt = uni(imin_(64, n_msg - base));  // SGPR: the loop test stays on the scalar unit
         for (int k = 0; k < cnt; ++k) {
             if (RC) B.mi = base + k;
             process_msg<RC>(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
@@ -2129,24 +2136,26 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     i32 prev_a = -1, prev_b = -1;
     float mid_acc = 0.0f, pa_acc = 0.0f, pb_acc = 0.0f;
     i32 last_p_a = 0, last_p_b = 0, last_t0 = 0, last_t1 = 0;
+    int4 nx = px, ny = py;  // the chunk's data rows, loaded one chunk ahead (chunk 0's at kernel start)
     for (int base = 0; base < M; base += 64) {
         const int row = base + l;
-        int4 x = make_int4(0, 0, 0, 0), y = x;
+        int4 x = nx, y = ny;
         if (row < AR) {
             x = reinterpret_cast<const int4*>(rows + row * 8)[0];
             y = reinterpret_cast<const int4*>(rows + row * 8)[1];
-        } else if (base == 0) {
-            x = px;
-            y = py;
-        } else if (row < M) {
-            const i32* g = msg_data + (size_t)(dstart + row - AR) * 8;
-            x = reinterpret_cast<const int4*>(g)[0];
-            y = reinterpret_cast<const int4*>(g)[1];
-            if (ftime) fixed_time_mask(x, y, t_end);
+        } else if (ftime && base > 0) {
+            fixed_time_mask(x, y, t_end);
+        }
+        nx = make_int4(0, 0, 0, 0);
+        ny = nx;
+        if ((row + 64 >= AR) & (row + 64 < M)) {  // the next chunk's loads land while this one runs
+            const i32* g = msg_data + (size_t)(dstart + row + 64 - AR) * 8;
+            nx = reinterpret_cast<const int4*>(g)[0];
+            ny = reinterpret_cast<const int4*>(g)[1];
         }
         decode_msgs(B.c, x, y);
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
-        const int cnt = imin_(64, M - base);
+        const int cnt = uni(imin_(64, M - base));  // SGPR: the loop test stays on the scalar unit
         for (int k = 0; k < cnt; ++k) {
             if (RC) B.mi = base + k;
             process_msg<RC>(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
