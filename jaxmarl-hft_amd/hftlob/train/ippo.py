@@ -21,6 +21,11 @@ One network (and optimizer) per agent type, as the reference:
   its own env shard; gradients are averaged with one all-reduce per agent type
   and minibatch (``torch.distributed``, RCCL on ROCm).
 
+On the GPU each minibatch step (forward over the sequence, loss, backward,
+clipping, Adam) is captured once per agent type in a HIP graph and replayed
+(``CUDA_GRAPHS``, single-process runs): a 64-step GRU unroll is thousands of small
+kernels, and replaying them as one graph removes their launch cost.
+
 Differences that are not semantics of the env: action sampling and parameter
 initialisation draw from torch's generator, not JAX's threefry, and the network
 runs through torch (rocBLAS GEMMs) rather than XLA.
@@ -50,7 +55,8 @@ def default_config(**kw) -> Dict:
     c = {"LR": [2.5e-4, 2.5e-4], "NUM_ENVS": 4096, "NUM_STEPS": 64, "GRU_HIDDEN_DIM": 256, "FC_DIM_SIZE": 256,
          "TOTAL_TIMESTEPS": 5e8, "UPDATE_EPOCHS": 4, "NUM_MINIBATCHES": 4, "GAMMA": [0.999999999, 0.999],
          "GAE_LAMBDA": [0.85, 0.9], "CLIP_EPS": 0.2, "ENT_COEF": [0.01, 0.01], "VF_COEF": [0.5, 0.5],
-         "MAX_GRAD_NORM": [0.5, 0.5], "ANNEAL_LR": [True, True], "NUM_AGENTS_PER_TYPE": [1, 1], "SEED": 2}
+         "MAX_GRAD_NORM": [0.5, 0.5], "ANNEAL_LR": [True, True], "NUM_AGENTS_PER_TYPE": [1, 1], "SEED": 2,
+         "CUDA_GRAPHS": True}
     c.update(kw)
     return c
 
@@ -76,14 +82,26 @@ class ActorCriticRNN(nn.Module):
         return h, self.actor2(F.relu(self.actor1(h))), v
 
     def forward(self, h0: torch.Tensor, obs: torch.Tensor, dones: torch.Tensor):
-        """A sequence [T, B, ...] from carry h0 (the ScannedRNN scan): logits [T, B, A], values [T, B]."""
-        logits, values = [], []
+        """A sequence [T, B, ...] from carry h0 (the ScannedRNN scan): logits [T, B, A], values [T, B].
+        The same cell as ``step``; the input-side GEMMs (embedding, the GRU's input
+        projection, both heads) run once over all T, only h @ W_hh stays in the scan."""
+        # unbind / chunk (not slicing): their backward concatenates the per-step grads once,
+        # where a slice's backward would zero-fill and add a whole [T, B, 3H] grad per step
+        gis = F.linear(F.relu(self.embed(obs)), self.gru.weight_ih, self.gru.bias_ih).unbind(0)  # (r, z, n)
+        w_hh, b_hh = self.gru.weight_hh, self.gru.bias_hh
         h = h0
-        for t in range(obs.shape[0]):
-            h, lg, v = self.step(h, obs[t], dones[t])
-            logits.append(lg)
-            values.append(v)
-        return torch.stack(logits), torch.stack(values)
+        hs = []
+        for t, gi in enumerate(gis):
+            h = torch.where(dones[t][:, None], torch.zeros_like(h), h)
+            ir, iz, i_n = gi.chunk(3, -1)
+            hr, hz, hn = F.linear(h, w_hh, b_hh).chunk(3, -1)
+            r = torch.sigmoid(ir + hr)
+            z = torch.sigmoid(iz + hz)
+            n = torch.tanh(i_n + r * hn)
+            h = (1.0 - z) * n + z * h
+            hs.append(h)
+        hseq = torch.stack(hs)
+        return self.actor2(F.relu(self.actor1(hseq))), self.critic2(F.relu(self.critic1(hseq))).squeeze(-1)
 
 
 @dataclass
@@ -171,7 +189,15 @@ class IPPOTrainer:
         torch.manual_seed(c["SEED"])  # the same initial parameters on every rank
         self.nets = [ActorCriticRNN(env.observation_spaces[i].shape[0], env.action_spaces[i].n, c["FC_DIM_SIZE"],
                                     c["GRU_HIDDEN_DIM"]).to(self.device) for i in range(nt)]
-        self.opts = [torch.optim.Adam(n.parameters(), lr=c["LR"][i], eps=1e-5) for i, n in enumerate(self.nets)]
+        world = dist.get_world_size() if dist is not None else 1
+        # HIP-graph minibatch steps: single process on the GPU (the grad all-reduce stays eager)
+        self.graphs = bool(c.get("CUDA_GRAPHS", False)) and self.device.type == "cuda" and world == 1
+        if self.graphs:  # capturable Adam: step counter and lr live on the device
+            self.opts = [torch.optim.Adam(n.parameters(), lr=torch.tensor(c["LR"][i], device=self.device), eps=1e-5,
+                                          capturable=True) for i, n in enumerate(self.nets)]
+        else:
+            self.opts = [torch.optim.Adam(n.parameters(), lr=c["LR"][i], eps=1e-5) for i, n in enumerate(self.nets)]
+        self._mb = [None] * nt   # per type: (graph, static inputs, static stats) once captured
         self.opt_count = [0] * nt
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(c["SEED"] + 1000 * (dist.get_rank() if dist is not None else 0))
@@ -226,6 +252,57 @@ class IPPOTrainer:
                 self.last_obs[i].copy_(obs[i].reshape(self.n_actors[i], -1))
                 self.last_done[i].copy_(dones["agents"][i].reshape(-1))
 
+    def _static(self, i: int, n: int, mb: int):
+        """Fixed-address inputs of agent type i's minibatch step (what a captured graph reads)."""
+        if not hasattr(self, "_st"):
+            self._st = [None] * self.n_types
+        if self._st[i] is None:
+            T, H = self.T, self.c["GRU_HIDDEN_DIM"]
+            self._st[i] = {"h0": torch.empty((n, H), device=self.device),
+                           "adv": torch.empty((T, n), device=self.device),
+                           "tgt": torch.empty((T, n), device=self.device),
+                           "idx": torch.zeros(n // mb, dtype=torch.long, device=self.device),
+                           "warm": 0, "graph": None, "out": None}
+        return self._st[i]
+
+    def _mb_step(self, i: int) -> torch.Tensor:
+        """One PPO minibatch step of agent type i from the static inputs: forward over the
+        sequences, loss, backward, grad pmean (multi-rank), global-norm clip, Adam."""
+        c, net, opt, b, st = self.c, self.nets[i], self.opts[i], self.buf[i], self._st[i]
+        idx = st["idx"]
+        logits, values = net(st["h0"][idx], b.obs[:, idx], b.done[:, idx])
+        out = ppo_loss(logits, values, b.action[:, idx], b.value[:, idx], b.log_prob[:, idx],
+                       st["adv"][:, idx], st["tgt"][:, idx], c["CLIP_EPS"], c["VF_COEF"][i], c["ENT_COEF"][i])
+        out[0].backward()
+        if self.dist is not None and self.dist.get_world_size() > 1:
+            _average_grads(list(net.parameters()), self.dist)
+        torch.nn.utils.clip_grad_norm_(net.parameters(), c["MAX_GRAD_NORM"][i])
+        opt.step()
+        return torch.stack([x.detach() for x in out])
+
+    def _minibatch(self, i: int) -> torch.Tensor:
+        st, opt = self._st[i], self.opts[i]
+        if not self.graphs:
+            opt.zero_grad(set_to_none=True)
+            return self._mb_step(i)
+        if st["graph"] is None and st["warm"] < 2:  # eager steps on a side stream before capture
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                opt.zero_grad(set_to_none=True)
+                r = self._mb_step(i)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            st["warm"] += 1
+            return r
+        if st["graph"] is None:  # capture once (nothing runs), then replay below
+            opt.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st["out"] = self._mb_step(i)
+            st["graph"] = g
+        st["graph"].replay()
+        return st["out"].clone()
+
     def update(self) -> Dict:
         """One _update_step: rollout, GAE, UPDATE_EPOCHS x NUM_MINIBATCHES PPO steps per agent type."""
         c = self.c
@@ -234,11 +311,13 @@ class IPPOTrainer:
         metrics = {"loss": [], "avg_reward": []}
         for i, net in enumerate(self.nets):
             b = self.buf[i]
+            n, mb = self.n_actors[i], c["NUM_MINIBATCHES"]
+            st = self._static(i, n, mb)
             with torch.no_grad():
                 _, _, last_val = net.step(self.h[i], self.last_obs[i], self.last_done[i])
                 adv, targets = calculate_gae(b.reward, b.value, b.global_done, last_val, c["GAMMA"][i],
                                              c["GAE_LAMBDA"][i])
-            n, mb = self.n_actors[i], c["NUM_MINIBATCHES"]
+                st["h0"].copy_(h0[i]); st["adv"].copy_(adv); st["tgt"].copy_(targets)
             stats = torch.zeros(6, device=self.device)
             for _ in range(c["UPDATE_EPOCHS"]):
                 perm = torch.randperm(n, device=self.device, generator=self.gen)
@@ -246,18 +325,13 @@ class IPPOTrainer:
                     if c["ANNEAL_LR"][i]:
                         lr = linear_schedule(c["LR"][i], self.opt_count[i], mb, c["UPDATE_EPOCHS"], self.num_updates)
                         for g in self.opts[i].param_groups:
-                            g["lr"] = lr
-                    logits, values = net(h0[i][idx], b.obs[:, idx], b.done[:, idx])
-                    out = ppo_loss(logits, values, b.action[:, idx], b.value[:, idx], b.log_prob[:, idx],
-                                   adv[:, idx], targets[:, idx], c["CLIP_EPS"], c["VF_COEF"][i], c["ENT_COEF"][i])
-                    self.opts[i].zero_grad(set_to_none=True)
-                    out[0].backward()
-                    if self.dist is not None and self.dist.get_world_size() > 1:
-                        _average_grads(list(net.parameters()), self.dist)
-                    torch.nn.utils.clip_grad_norm_(net.parameters(), c["MAX_GRAD_NORM"][i])
-                    self.opts[i].step()
+                            if torch.is_tensor(g["lr"]):
+                                g["lr"].fill_(lr)
+                            else:
+                                g["lr"] = lr
+                    st["idx"].copy_(idx)
+                    stats += self._minibatch(i)
                     self.opt_count[i] += 1
-                    stats += torch.stack([x.detach() for x in out])
             stats /= c["UPDATE_EPOCHS"] * mb
             metrics["loss"].append(dict(zip(("total_loss", "value_loss", "actor_loss", "entropy", "approx_kl",
                                              "clip_frac"), stats)))
