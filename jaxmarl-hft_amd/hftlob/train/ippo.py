@@ -197,7 +197,7 @@ class IPPOTrainer:
                                           capturable=True) for i, n in enumerate(self.nets)]
         else:
             self.opts = [torch.optim.Adam(n.parameters(), lr=c["LR"][i], eps=1e-5) for i, n in enumerate(self.nets)]
-        self._mb = [None] * nt   # per type: (graph, static inputs, static stats) once captured
+        self._roll = None        # the captured rollout graph (False: not capturable, stays eager)
         self.opt_count = [0] * nt
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(c["SEED"] + 1000 * (dist.get_rank() if dist is not None else 0))
@@ -225,19 +225,48 @@ class IPPOTrainer:
     def _next_keys(self) -> torch.Tensor:
         """rng, _rng = split(rng); rng_step = split(_rng, NUM_ENVS) (:613-614)."""
         k = self._split(self.rng[None], 2)[0]
-        self.rng = k[0].clone()
+        self.rng.copy_(k[0])
         return self._split(k[1:2].contiguous(), self.E)[0].contiguous()
 
     @torch.no_grad()
     def rollout(self) -> None:
-        """NUM_STEPS of _env_step (:578-658), all on the device."""
+        """NUM_STEPS of _env_step (:578-658), all on the device; with CUDA_GRAPHS the whole
+        rollout (policy, sampling, env steps, buffer writes) is one captured HIP graph."""
+        if not self.graphs or self._roll is False:
+            return self._rollout()
+        if self._roll is None:  # one eager rollout (warm-up), then capture; capture runs nothing
+            self._rollout_side()
+            self._roll = 0
+            return None
+        if self._roll == 0:
+            g = torch.cuda.CUDAGraph()
+            g.register_generator_state(self.gen)
+            try:
+                with torch.cuda.graph(g):
+                    self._rollout()
+            except RuntimeError:  # an op that cannot be captured: stay eager
+                self._roll = False
+                return self._rollout()
+            self._roll = g
+        self._roll.replay()
+        return None
+
+    def _rollout_side(self) -> None:
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self._rollout()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+
+    def _rollout(self) -> None:
         for t in range(self.T):
             actions = []
             for i, net in enumerate(self.nets):
                 b = self.buf[i]
                 b.obs[t].copy_(self.last_obs[i])
                 b.done[t].copy_(self.last_done[i])
-                self.h[i], logits, v = net.step(self.h[i], self.last_obs[i], self.last_done[i])
+                h, logits, v = net.step(self.h[i], self.last_obs[i], self.last_done[i])
+                self.h[i].copy_(h)
                 probs = torch.softmax(logits, -1)
                 a = torch.multinomial(probs, 1, generator=self.gen).squeeze(-1)
                 b.action[t].copy_(a)
