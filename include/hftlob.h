@@ -80,7 +80,7 @@ enum { HFTLOB_INVPEN_NONE = 0, HFTLOB_INVPEN_LINEAR, HFTLOB_INVPEN_QUADRATIC,
 enum { HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX = 0, HFTLOB_EXE_ACT_SIMPLEST_CASE = 1, HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG = 2,
        HFTLOB_EXE_ACT_TWAP = 3, HFTLOB_EXE_ACT_FIXED_PRICES = 4 };
 enum { HFTLOB_EXE_OBS_ENGINEERED = 0, HFTLOB_EXE_OBS_BASIC = 1, HFTLOB_EXE_OBS_SIMPLEST_CASE = 2 };
-enum { HFTLOB_EXE_REW_NORMAL = 0, HFTLOB_EXE_REW_FINISH_FAST = 1 };
+enum { HFTLOB_EXE_REW_NORMAL = 0, HFTLOB_EXE_REW_FINISH_FAST = 1, HFTLOB_EXE_REW_SIMPLEST_CASE = 2 };
 enum { HFTLOB_TASK_RANDOM = 0, HFTLOB_TASK_BUY = 1, HFTLOB_TASK_SELL = 2 };
 
 /* One agent type (one entry of MultiAgentConfig.dict_of_agents_configs). */

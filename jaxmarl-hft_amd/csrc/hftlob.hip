@@ -1850,6 +1850,16 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     R.quant_left = wsub(wsub(task, qe), aq);
     R.reward_info = reward;
     if (tc.reward_function == HFTLOB_EXE_REW_FINISH_FAST) reward = i2f(wsub(0, iabs_(R.quant_left)));
+    if (tc.reward_function == HFTLOB_EXE_REW_SIMPLEST_CASE) {  // :1723-1731: sum (p - init_price) |q|, sign by task
+        float ps[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const bool mine = V.valid[r] && (tid == V.PT[r] || tid == V.AT[r]);
+            const float slip = i2f(mine ? V.P[r] : 0) - init_price;
+            ps[r] = (sell ? slip : -slip) * i2f(mine ? iabs_(V.Q[r]) : 0);
+        }
+        reward = rows_fsum(ps, nT);
+    }
     R.reward = reward; R.p_vwap = pv; R.advantage = adv; R.drift = drift; R.slippage = slip;
     R.agentQuant = aq; R.qp_agent = qp;
 }

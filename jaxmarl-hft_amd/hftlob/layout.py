@@ -85,7 +85,7 @@ PRICE = {"mid": 0, "mid_avg": 1, "far_touch": 2, "near_touch": 3}
 INV_PEN = {"none": 0, "linear": 1, "quadratic": 2, "threshold": 3}
 EXE_ACTION = {"fixed_quants_complex": 0, "simplest_case": 1, "fixed_quants_1msg": 2, "twap": 3, "fixed_prices": 4}
 EXE_OBS = {"engineered": 0, "basic": 1, "simplest_case": 2}
-EXE_REWARD = {"normal": 0, "finish_fast": 1}
+EXE_REWARD = {"normal": 0, "finish_fast": 1, "simplest_case": 2}
 TASK = {"random": 0, "buy": 1, "sell": 2}
 
 MM_WORDS = ("posted_distance_bid", "posted_distance_ask", "inventory", "total_PnL", "cash_balance")

@@ -1125,6 +1125,18 @@ static void exe_reward(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc,
     R->quant_left = wsub(wsub(task, qe), aq);
     R->reward_info = reward; /* info["reward"] is taken before the finish_fast override */
     if (tc->reward_function == HFTLOB_EXE_REW_FINISH_FAST) reward = i2f(wsub(0, iabs(R->quant_left)));
+    if (tc->reward_function == HFTLOB_EXE_REW_SIMPLEST_CASE) { /* exec_env.py:1723-1731 */
+        float ps[HFTLOB_MAX_SLOTS];
+        for (int i = 0; i < nT; ++i) {
+            const i32* r = tr + i * 8;
+            int valid = r[0] >= 0;
+            int mine = valid && (tid == r[6] || tid == r[7]);
+            /* agentTrades rows are 0 outside the agent's executed trades: price_slip = 0 - init_price there */
+            float slip = i2f(mine ? r[0] : 0) - init_price;
+            ps[i] = (sell ? slip : -slip) * i2f(mine ? iabs(r[1]) : 0);
+        }
+        reward = wsum(ps, nT);
+    }
     R->reward = reward;
     R->p_vwap = pv;
     R->advantage = adv;

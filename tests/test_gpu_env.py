@@ -213,6 +213,7 @@ def test_mm_avst_fixed_time(tmp_path_factory):
 
 
 EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid", task="buy"),
+                dict(reward_function="simplest_case"), dict(reward_function="simplest_case", task="buy"),
                 dict(task="sell", normalize=False),
                 dict(doom_price_penalty=0.1),                    # Python-float penalty: f32 far-touch price
                 dict(doom_price_penalty=0.37, reference_price="mid"),
