@@ -76,7 +76,7 @@ enum { HFTLOB_MM_REW_PORTFOLIO_VALUE = 0, HFTLOB_MM_REW_BUY_SELL_PNL, HFTLOB_MM_
 enum { HFTLOB_PRICE_MID = 0, HFTLOB_PRICE_MID_AVG = 1, HFTLOB_PRICE_FAR_TOUCH = 2,
        HFTLOB_PRICE_NEAR_TOUCH = 3 };
 enum { HFTLOB_INVPEN_NONE = 0, HFTLOB_INVPEN_LINEAR, HFTLOB_INVPEN_QUADRATIC,
-       HFTLOB_INVPEN_THRESHOLD };
+       HFTLOB_INVPEN_THRESHOLD, HFTLOB_INVPEN_EXP4 };
 enum { HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX = 0, HFTLOB_EXE_ACT_SIMPLEST_CASE = 1, HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG = 2,
        HFTLOB_EXE_ACT_TWAP = 3, HFTLOB_EXE_ACT_FIXED_PRICES = 4 };
 enum { HFTLOB_EXE_OBS_ENGINEERED = 0, HFTLOB_EXE_OBS_BASIC = 1, HFTLOB_EXE_OBS_SIMPLEST_CASE = 2 };

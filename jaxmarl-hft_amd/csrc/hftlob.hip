@@ -1757,6 +1757,8 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     else if (tc.inv_penalty == HFTLOB_INVPEN_THRESHOLD)
         inv_pen = i2f(iabs_(new_inv)) > tc.inv_penalty_threshold
                       ? -1.0f * (i2f(wmul(new_inv, new_inv)) / tc.inv_penalty_quadratic_factor) : 0.0f;
+    else if (tc.inv_penalty == HFTLOB_INVPEN_EXP4)  // mm_env.py:2528-2529: -exp(inv * 4), int32 product
+        inv_pen = -1.0f * expf(i2f(wmul(new_inv, 4)));
     reward = reward + tc.inv_penalty_lambda * inv_pen;
     if (tc.clip_reward) reward = fminf(fmaxf(reward, -10000.0f), 10000.0f);
     if (tc.volume_traded_bonus == 1) reward = reward + fabsf(reward) * market_share;

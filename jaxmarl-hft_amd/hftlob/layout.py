@@ -82,7 +82,7 @@ MM_REWARD = {"portfolio_value": 0, "buy_sell_pnl": 1, "complex": 2, "zero_inv": 
              "spooner_damped": 5, "spooner_asym_damped": 6, "spooner_asym_damped2": 7,
              "spooner_scaled": 8, "delta_portfolio_value": 9}
 PRICE = {"mid": 0, "mid_avg": 1, "far_touch": 2, "near_touch": 3}
-INV_PEN = {"none": 0, "linear": 1, "quadratic": 2, "threshold": 3}
+INV_PEN = {"none": 0, "linear": 1, "quadratic": 2, "threshold": 3, "exp4": 4}
 EXE_ACTION = {"fixed_quants_complex": 0, "simplest_case": 1, "fixed_quants_1msg": 2, "twap": 3, "fixed_prices": 4}
 EXE_OBS = {"engineered": 0, "basic": 1, "simplest_case": 2}
 EXE_REWARD = {"normal": 0, "finish_fast": 1, "simplest_case": 2}

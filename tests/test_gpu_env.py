@@ -173,6 +173,7 @@ MM_VARIANTS = [
     dict(reference_price="far_touch", unwind_price="far_touch"),
     dict(reference_price="near_touch", inv_penalty="linear"),
     dict(inv_penalty="quadratic", clip_reward=True),
+    dict(inv_penalty="exp4", inv_penalty_lambda=1e-6),
     dict(inv_penalty="threshold", exclude_extreme_spreads=True, volume_traded_bonus="market_share"),
     dict(auto_liquidate_threshold=3, normalize=False),
 ]
