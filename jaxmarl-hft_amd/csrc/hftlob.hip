@@ -1012,12 +1012,29 @@ struct WorldView {  // wave-uniform world quantities used by obs
 };
 
 // MM _get_obs_basic / _get_obs_engineered (fixed_steps), sorted keys — mm_env.py:2963-3154
-DEV void mm_obs(const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o) {
+DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o,
+                bool ftime) {
     const bool nz = tc.normalize;
     const i32 spread = iabs_(wsub(w.best_ask_p, w.best_bid_p));
     if (tc.observation_space == HFTLOB_MM_OBS_BASIC) {
         o[0] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
         o[1] = nz ? i2f(spread) / 1e4f : i2f(spread);
+        return;
+    }
+    if (ftime) {  // mm_env.py:3029-3088, sorted keys: delta_time, inventory, mid_price, p_ask, p_bid, q_ask,
+                  // q_bid, spread, step_counter, time_remaining
+        const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
+        const float trem = (float)c.episode_time - (tm - (i2f(w.it0) + i2f(w.it1) / 1e9f));
+        o[0] = nz ? w.dt / 10.0f : w.dt;
+        o[1] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
+        o[2] = nz ? w.mid / 1e6f : w.mid;
+        o[3] = nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p);
+        o[4] = nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p);
+        o[5] = nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a);
+        o[6] = nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b);
+        o[7] = nz ? i2f(spread) / 1e4f : i2f(spread);
+        o[8] = nz ? i2f(w.step) / 10.0f : i2f(w.step);
+        o[9] = nz ? trem / (float)c.episode_time : trem;
         return;
     }
     o[0] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
@@ -1113,7 +1130,7 @@ DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     float o[HFTLOB_MAX_OBS];
 #pragma unroll
     for (int k = 0; k < HFTLOB_MAX_OBS; ++k) o[k] = 0.0f;
-    if (tc.kind == HFTLOB_AGENT_MM) mm_obs(tc, w, st, o);
+    if (tc.kind == HFTLOB_AGENT_MM) mm_obs(c, tc, w, st, o, ftime);
     else exe_obs(c, tc, w, st, o, ftime);
     const int l = lane_id();
     float v = 0.0f;

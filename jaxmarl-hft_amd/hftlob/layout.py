@@ -119,12 +119,12 @@ EP_TYPE = {"fixed_steps": 0, "fixed_time": 1}
 
 
 def obs_dim(agent_cfg, world) -> int:
-    """observation_space() widths: mm_env.py (basic 2, engineered 8, both episode types);
+    """observation_space() widths: mm_env.py:3195-3200 (basic 2; engineered 8 fixed_steps, 10 fixed_time);
     exec_env.py:2185-2200 (engineered: 12 fixed_steps, 15 fixed_time)."""
     if world.ep_type not in EP_TYPE:
         raise ValueError(f"ep_type {world.ep_type!r}: use 'fixed_steps' or 'fixed_time'")
     if isinstance(agent_cfg, MarketMaking_EnvironmentConfig):
-        return {"basic": 2, "engineered": 8}[agent_cfg.observation_space]
+        return {"basic": 2, "engineered": 8 if world.ep_type == "fixed_steps" else 10}[agent_cfg.observation_space]
     return {"engineered": 12 if world.ep_type == "fixed_steps" else 15, "basic": 3,
             "simplest_case": 3}[agent_cfg.observation_space]
 

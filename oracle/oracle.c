@@ -1161,6 +1161,18 @@ static void mm_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env
         o[1] = nrm(i2f(spread), 1e4f, nz);
         return;
     }
+    if (c->ep_type == 1) { /* mm_env.py:3029-3088: 10 sorted keys */
+        const i32* W = WORLD(E);
+        const i32* L = LOADED(E);
+        float tm = i2f(W[0]) + i2f(W[1]) / 1e9f;
+        float time_elapsed = tm - (i2f(L[0]) + i2f(L[1]) / 1e9f);
+        float time_remaining = (float)c->episode_time - time_elapsed;
+        float v[10] = {bitf(W[4]), i2f(st[2]), bitf(W[3]), i2f(pa), i2f(pb), i2f(side_volume(ASKS(E), nO)),
+                       i2f(side_volume(BIDS(E), nO)), i2f(spread), i2f(L[5]), time_remaining};
+        float sd[10] = {10.0f, 10.0f, 1e6f, 1e6f, 1e6f, 1000.0f, 1000.0f, 1e4f, 10.0f, (float)c->episode_time};
+        for (int k = 0; k < 10; ++k) o[k] = nrm(v[k], sd[k], nz);
+        return;
+    }
     /* inventory, mid_price, p_ask, p_bid, q_ask, q_bid, spread, step_counter */
     o[0] = nrm(i2f(st[2]), 10.0f, nz);
     o[1] = nrm(bitf(WORLD(E)[3]), 1e6f, nz);

@@ -213,6 +213,18 @@ def test_mm_avst_fixed_time(tmp_path_factory):
     rollout_parity(cfg, E=32, K=20, day=day)
 
 
+@pytest.mark.parametrize("norm", [True, False])
+def test_mm_engineered_fixed_time(norm, tmp_path_factory):
+    """MM engineered obs under fixed_time episodes: 10 sorted keys incl. delta_time and
+    time_remaining (mm_env.py:3029-3088, observation_space :3195-3198)."""
+    day = _loaded("fixed_time", str(tmp_path_factory.mktemp("lob")))
+    cfg = builtin_config("2_player_fq_fqc")
+    w = dataclasses.replace(cfg.world_config, ep_type="fixed_time", episode_time=300, start_resolution=300)
+    cfg = variant(dataclasses.replace(cfg, world_config=w), "MarketMaking", observation_space="engineered",
+                  normalize=norm)
+    rollout_parity(cfg, E=32, K=20, day=day)
+
+
 EXE_VARIANTS = [dict(reward_function="finish_fast"), dict(reference_price="mid", task="buy"),
                 dict(reward_function="simplest_case"), dict(reward_function="simplest_case", task="buy"),
                 dict(task="sell", normalize=False),

@@ -164,3 +164,73 @@ def test_mm_action_messages_vs_numpy(changes):
         acts = O.sample_actions(c, keys + 7 * k)
         st = O.env_step(c, keys + 7 * k, acts, day.msgs, init, st)[0]
     assert checked > 100
+
+
+# ------------------------------------------------------------ MM observations
+def mm_obs_numpy(t, w, rec, L, a_off):
+    """_get_obs_basic (mm_env.py:2963-3000) / _get_obs_engineered (:3004-3154), normalize_obs
+    (:3157-3167), ravel_pytree key order, from the record the step produced."""
+    M = L.n_msgs
+    pa = int(rec[L.off_best_asks + 2 * (M - 1)])
+    pb = int(rec[L.off_best_bids + 2 * (M - 1)])
+    spread = abs(pa - pb)
+    inv = int(rec[a_off + 2])
+    if t.observation_space == "basic":
+        obs, std = {"inventory": inv, "spread": spread}, {"inventory": 10, "spread": 1e4}
+    else:
+        asks = rec[L.off_asks:L.off_asks + 6 * w.nOrders].reshape(-1, 6)
+        bids = rec[L.off_bids:L.off_bids + 6 * w.nOrders].reshape(-1, 6)
+        wr = rec[L.off_world:L.off_world + 5]
+        lr = rec[L.off_loaded:L.off_loaded + 6]
+        obs = {"p_bid": pb, "p_ask": pa, "spread": spread,
+               "q_bid": int(np.where(bids[:, 0] != -1, bids[:, 1], 0).sum()),
+               "q_ask": int(np.where(asks[:, 0] != -1, asks[:, 1], 0).sum()),
+               "mid_price": wr[3:4].view(np.float32)[0], "step_counter": int(lr[5]), "inventory": inv}
+        std = {"p_bid": 1e6, "p_ask": 1e6, "spread": 1e4, "q_bid": 1000, "q_ask": 1000, "mid_price": 1e6,
+               "step_counter": 10, "inventory": 10}
+        if w.ep_type == "fixed_time":
+            time = F(F(wr[0]) + F(wr[1]) / F(1e9))
+            elapsed = F(time - F(F(lr[0]) + F(lr[1]) / F(1e9)))
+            obs.update(delta_time=wr[4:5].view(np.float32)[0], time_remaining=F(F(w.episode_time) - elapsed))
+            std.update(delta_time=10, time_remaining=w.episode_time)
+    keys = sorted(obs)
+    if t.normalize:
+        return [F(F(obs[k]) / F(std[k])) for k in keys]
+    return [F(obs[k]) for k in keys]
+
+
+@pytest.mark.parametrize("obs_space,norm,ep", [("basic", True, "fixed_steps"), ("engineered", True, "fixed_steps"),
+                                               ("engineered", False, "fixed_steps"),
+                                               ("engineered", True, "fixed_time"), ("engineered", False, "fixed_time")])
+def test_mm_obs_vs_numpy(obs_space, norm, ep, tmp_path):
+    cfg = variant(builtin_config("2_player_fq_fqc"), "MarketMaking", observation_space=obs_space, normalize=norm)
+    if ep == "fixed_time":
+        import dataclasses
+        from hftlob.data import lobster as Lb
+        from hftlob.data.raw_synthetic import write_raw_lobster_day
+        w = dataclasses.replace(cfg.world_config, ep_type="fixed_time", episode_time=300, start_resolution=300)
+        cfg = dataclasses.replace(cfg, world_config=w)
+        write_raw_lobster_day(str(tmp_path), n_events=12_000, seed=3, mid=2_000_000)
+        ld = Lb.LoadLOBSTER_resample(str(tmp_path), str(tmp_path), 10, "fixed_time", window_length=300,
+                                     window_resolution=300, n_data_msg_per_step=100, stock="SYN",
+                                     time_period="2026_Oct")
+        day = Lb.LoadedDay.from_arrays(*ld.run_loading("cpu_ft"))
+    else:
+        w = cfg.world_config
+        day = generate_day(n_msgs=20_000, seed=6, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    w = cfg.world_config
+    t = cfg.dict_of_agents_configs["MarketMaking"]
+    win = make_windows(day, w)
+    c, L = pack_env_cfg(cfg, len(win.starts), day.msgs.shape[0], True)
+    init = O.init_states(c.lob, win, day.msgs, w, L.init_rec_words)
+    E = 8
+    keys = np.arange(2 * E, dtype=np.uint32).reshape(E, 2)
+    st, o = O.env_reset(c, keys, init)
+    d = L.obs_dims[0]
+    assert d == {"basic": 2, "engineered": 8 if ep == "fixed_steps" else 10}[obs_space]
+    for k in range(12):
+        for e in range(E):
+            want = mm_obs_numpy(t, w, st[e], L, L.agent_offsets[0])
+            assert np.array_equal(o[e, 0, :d], np.array(want, np.float32)), (k, e, o[e, 0, :d], want)
+        acts = O.sample_actions(c, keys + 3 * k)
+        st, o = O.env_step(c, keys + 3 * k, acts, day.msgs, init, st)[:2]
