@@ -776,6 +776,10 @@ DEV int random_id_match(const Book<S>& B, Key& k, const i32 (&o)[S], const lmask
 }
 // cancel_order + get_init_id_match — :93-139 (+ :141-164 when RC)
 template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+    // On clean sides (the !G variant) a zero-quantity cancel changes nothing: whichever row it
+    // picks keeps q (or, empty, stays all -1) and the best quote is unchanged.  The agents'
+    // unused cancel rows (getCancelMsgs' zero rows) are such messages.
+    if (!G && m.qty == 0) return;
     const int R = B.c.nO;
     i32 o[S], p[S], q[S];
     ldcol(s.t, R, FOID, o);
