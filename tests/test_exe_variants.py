@@ -229,3 +229,80 @@ def test_multidiscrete_sampling_vs_numpy(part):
         mm = R.randint(R.split(sub[0], 1, part)[0], 0, c.types[0].n_actions, part)
         exe = R.randint_vec(R.split(sub[1], 1, part)[0], 3, 0, 7, part)
         assert acts[e].tolist() == [mm] + exe
+
+
+# ------------------------------------------------- EXE engineered observation
+def exe_engineered_numpy(t, w, rec, L, a_off):
+    """_get_obs (exec_env.py:1913-2079) + normalize_obs (:2152-2162), sorted keys, from the record."""
+    M = L.n_msgs
+    ba = int(rec[L.off_best_asks + 2 * (M - 1)])
+    bb = int(rec[L.off_best_bids + 2 * (M - 1)])
+    asks = rec[L.off_asks:L.off_asks + 6 * w.nOrders].reshape(-1, 6)
+    bids = rec[L.off_bids:L.off_bids + 6 * w.nOrders].reshape(-1, 6)
+    va = int(np.where(asks[:, 0] != -1, asks[:, 1], 0).sum())
+    vb = int(np.where(bids[:, 0] != -1, bids[:, 1], 0).sum())
+    st = rec[a_off:a_off + 13]
+    init = rec[a_off:a_off + 1].view(np.float32)[0]
+    task, qe, sell = int(st[1]), int(st[2]), int(st[3])
+    pa, pp = (bb, ba) if sell else (ba, bb)
+    qa, qp = (vb, va) if sell else (va, vb)
+    wr, lr = rec[L.off_world:L.off_world + 5], rec[L.off_loaded:L.off_loaded + 6]
+    sc, ms = int(lr[5]), int(lr[3])
+    rr = F(0) if ms == 0 else F(F(1) - F(F(sc) / F(ms)))
+    obs = {"is_sell_task": (sell, 0, 1), "p_aggr": (pa, init, 1e5), "p_pass": (pp, init, 1e5),
+           "spread": (abs(pa - pp), 0, 1e4), "q_aggr": (qa, 0, 1000), "q_pass": (qp, 0, 1000),
+           "init_price": (init, 0, 1e7), "task_size": (task, 0, t.task_size), "executed_quant": (qe, 0, t.task_size),
+           "remaining_quant": (task - qe, 0, t.task_size), "step_counter": (sc, 0, 30), "remaining_ratio": (rr, 0, 1)}
+    if w.ep_type == "fixed_time":
+        time = F(F(wr[0]) + F(wr[1]) / F(1e9))
+        elapsed = F(time - F(F(lr[0]) + F(lr[1]) / F(1e9)))
+        obs.update(time=(time, 0, 1e5), delta_time=(wr[4:5].view(np.float32)[0], 0, 10),
+                   time_remaining=(F(F(w.episode_time) - elapsed), 0, w.episode_time))
+    out = []
+    for k in sorted(obs):
+        x, m, s = obs[k]
+        x = F(F(x) - F(m)) if isinstance(m, np.floating) else F(x)   # int - 0 stays exact
+        out.append(F(x / F(s)) if t.normalize else F(obs[k][0]))
+    return out
+
+
+@pytest.mark.parametrize("norm,ep,task", [(True, "fixed_steps", "random"), (False, "fixed_steps", "random"),
+                                          (True, "fixed_steps", "buy"), (True, "fixed_time", "random"),
+                                          (False, "fixed_time", "sell")])
+def test_exe_engineered_obs_vs_numpy(norm, ep, task, tmp_path):
+    import dataclasses
+    cfg = variant(builtin_config("2_player_fq_fqc"), "Execution", normalize=norm, task=task)
+    if ep == "fixed_time":
+        from hftlob.data import lobster as Lb
+        from hftlob.data.raw_synthetic import write_raw_lobster_day
+        w = dataclasses.replace(cfg.world_config, ep_type="fixed_time", episode_time=300, start_resolution=300)
+        cfg = dataclasses.replace(cfg, world_config=w)
+        write_raw_lobster_day(str(tmp_path), n_events=12_000, seed=3, mid=2_000_000)
+        ld = Lb.LoadLOBSTER_resample(str(tmp_path), str(tmp_path), 10, "fixed_time", window_length=300,
+                                     window_resolution=300, n_data_msg_per_step=100, stock="SYN",
+                                     time_period="2026_Oct")
+        day = Lb.LoadedDay.from_arrays(*ld.run_loading("cpu_ft"))
+    else:
+        w = cfg.world_config
+        day = generate_day(n_msgs=20_000, seed=6, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    w = cfg.world_config
+    t = cfg.dict_of_agents_configs["Execution"]
+    win = make_windows(day, w)
+    c, L = pack_env_cfg(cfg, len(win.starts), day.msgs.shape[0], True)
+    init = O.init_states(c.lob, win, day.msgs, w, L.init_rec_words)
+    E = 8
+    keys = np.arange(2 * E, dtype=np.uint32).reshape(E, 2) + 11
+    st, o = O.env_reset(c, keys, init)
+    d = L.obs_dims[1]
+    assert d == (12 if ep == "fixed_steps" else 15)
+    dn = np.zeros((E, 2), np.int32)
+    da = np.zeros(E, np.int32)
+    for k in range(14):
+        for e in range(E):
+            if dn[e, 1] and not da[e]:          # done agent, episode running: obs zeroed (marl_env.py:690-699)
+                assert not o[e, 1, :d].any()
+                continue
+            want = exe_engineered_numpy(t, w, st[e], L, L.agent_offsets[1])
+            assert np.array_equal(o[e, 1, :d], np.array(want, np.float32)), (k, e, o[e, 1, :d], want)
+        acts = O.sample_actions(c, keys + 3 * k)
+        st, o, _, da, dn, _ = O.env_step(c, keys + 3 * k, acts, day.msgs, init, st)
