@@ -1345,12 +1345,25 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
     const bool empty = masked_best(c, B, tid, last_ba, last_bb, ba, bb);
     const float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
     const float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
-    const int ai = action < 0 ? imax_(action + 10, 0) : (action > 9 ? 9 : action);  // jnp gather index
-    // offsets tables {0,1,2,3,4,0,2,5,1,0} / {0,1,2,3,4,2,0,1,5,0}; quants 1.. ,0
-    const float bo = (float)((0x0152043210ull >> (4 * ai)) & 0xF);
-    const float ao = (float)((0x0510243210ull >> (4 * ai)) & 0xF);
-    const i32 q1 = ai == 9 ? 0 : 1;
-    i32 bq = wmul(q1, tc.fixed_quant_value), aq = wmul(q1, tc.fixed_quant_value);
+    float bo, ao;
+    i32 bq, aq;
+    if (!tc.sell_buy_all_option) {
+        const int ai = action < 0 ? imax_(action + 10, 0) : (action > 9 ? 9 : action);  // jnp gather index
+        // offsets tables {0,1,2,3,4,0,2,5,1,0} / {0,1,2,3,4,2,0,1,5,0}; quants 1.. ,0
+        bo = (float)((0x0152043210ull >> (4 * ai)) & 0xF);
+        ao = (float)((0x0510243210ull >> (4 * ai)) & 0xF);
+        const i32 q1 = ai == 9 ? 0 : 1;
+        bq = wmul(q1, tc.fixed_quant_value);
+        aq = wmul(q1, tc.fixed_quant_value);
+    } else {  // mm_env.py:1018-1023: 9-entry tables, entries 6 / 7 sell or buy the inventory back
+        const int ai = action < 0 ? imax_(action + 9, 0) : (action > 8 ? 8 : action);
+        const i32 bot[9] = {10, 2, 4, -1, 0, 2, -20, 0, 0}, aot[9] = {10, 2, 4, -1, 2, 0, 0, -20, 0};
+        const i32 iq = ifloordiv(st[2], tc.fixed_quant_value);
+        bo = i2f(bot[ai]);
+        ao = i2f(aot[ai]);
+        bq = wmul(ai < 6 ? 1 : (ai == 6 ? iq : 0), tc.fixed_quant_value);
+        aq = wmul(ai < 6 ? 1 : (ai == 7 ? iq : 0), tc.fixed_quant_value);
+    }
     if (empty) { bq = 0; aq = 0; }
     const float bpf = i2f(bb) - bo * hs;
     const float apf = i2f(ba) + ao * hs;
@@ -2461,8 +2474,6 @@ static int check_env(const hftlob_env_cfg* c) {
         const hftlob_agent_type_cfg& tc = c->types[t];
         agents += tc.n_agents;
         if (tc.kind == HFTLOB_AGENT_MM) {
-            if (tc.sell_buy_all_option && tc.action_space != HFTLOB_MM_ACT_SIMPLE)
-                return fail(HFTLOB_EINVAL, "MM sell_buy_all_option: simple action space only");
             if (tc.action_space < 0 || tc.action_space > HFTLOB_MM_ACT_SIMPLE) return fail(HFTLOB_EINVAL, "MM action_space");
             if ((tc.action_space == HFTLOB_MM_ACT_BOB_RL || tc.action_space == HFTLOB_MM_ACT_BOB_STRATEGY) &&
                 tc.bob_v0 <= 0)

@@ -225,8 +225,6 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
             raise ValueError("Invalid reward_space specified.")
         if t.inv_penalty not in INV_PEN:
             raise NotImplementedError(f"inv_penalty {t.inv_penalty!r} not implemented")
-        if t.sell_buy_all_option and t.action_space not in ("simple",):
-            raise NotImplementedError("sell_buy_all_option=True is implemented for the 'simple' action space")
         if t.action_space == "spread_skew" and t.multiplier_type not in ("tick", "spread"):
             raise ValueError(f"multiplier_type {t.multiplier_type!r}")
         if t.unwind_price not in ("mid", "mid_avg", "far_touch"):

@@ -552,9 +552,21 @@ static void mm_fixed_quant(const hftlob_env_cfg* c, const hftlob_agent_type_cfg*
     if (empty) { bb = BBIDS(E)[(c->n_msgs - 1) * 2]; ba = BASKS(E)[(c->n_msgs - 1) * 2]; }
     float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
     float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
-    int ai = gather_idx(action, 10); /* jnp gather: negative wraps, then clamps */
-    float bo = boff[ai], ao = aoff[ai];
-    i32 bquant = wmul(bq[ai], tc->fixed_quant_value), aquant = wmul(aq[ai], tc->fixed_quant_value);
+    float bo, ao;
+    i32 bquant, aquant;
+    if (!tc->sell_buy_all_option) {
+        int ai = gather_idx(action, 10); /* jnp gather: negative wraps, then clamps */
+        bo = boff[ai]; ao = aoff[ai];
+        bquant = wmul(bq[ai], tc->fixed_quant_value); aquant = wmul(aq[ai], tc->fixed_quant_value);
+    } else { /* mm_env.py:1018-1023 */
+        static const float boff9[9] = {10, 2, 4, -1, 0, 2, -20, 0, 0};
+        static const float aoff9[9] = {10, 2, 4, -1, 2, 0, 0, -20, 0};
+        i32 iq = ifloordiv(st[2], tc->fixed_quant_value);
+        i32 bq9[9] = {1, 1, 1, 1, 1, 1, iq, 0, 0}, aq9[9] = {1, 1, 1, 1, 1, 1, 0, iq, 0};
+        int ai = gather_idx(action, 9);
+        bo = boff9[ai]; ao = aoff9[ai];
+        bquant = wmul(bq9[ai], tc->fixed_quant_value); aquant = wmul(aq9[ai], tc->fixed_quant_value);
+    }
     if (empty) { bquant = 0; aquant = 0; }
     float bpf = i2f(bb) - bo * hs;
     float apf = i2f(ba) + ao * hs;
@@ -1337,7 +1349,6 @@ static int env_cfg_ok(const hftlob_env_cfg* c) {
     int words = 0;
     for (int t = 0; t < c->n_types; ++t) {
         const hftlob_agent_type_cfg* tc = &c->types[t];
-        if (tc->kind == HFTLOB_AGENT_MM && tc->sell_buy_all_option && tc->action_space != HFTLOB_MM_ACT_SIMPLE) return 0;
         if (tc->kind == HFTLOB_AGENT_EXE && tc->action_space == HFTLOB_EXE_ACT_FIXED_PRICES &&
             (tc->n_actions < 1 || tc->n_actions > 4 || tc->action_width != tc->n_actions))
             return 0;

@@ -106,7 +106,6 @@ def test_error_bad_env_cfg(L):
                          (lambda c: setattr(c, "n_agents", 3), -1),
                          (lambda c: setattr(c, "n_msgs", 1000), -3),
                          (lambda c: setattr(c.types[0], "kind", 7), -1),
-                         (lambda c: setattr(c.types[0], "sell_buy_all_option", 1), -1),
                          (lambda c: setattr(c, "action_words", 3), -1),
                          (lambda c: setattr(c.types[0], "action_width", 2), -1),
                          (lambda c: setattr(c.types[1], "action_space", 4), -1),     # fixed_prices, width 1 != 13

@@ -64,7 +64,6 @@ def test_roundtrip(tmp_path, fmt):
 @pytest.mark.parametrize("agent,changes,err", [
     ("MarketMaking", dict(action_space="fixed_prices"), NotImplementedError),   # reference NameError
     ("MarketMaking", dict(action_space="bogus"), ValueError),
-    ("MarketMaking", dict(action_space="bobRL", sell_buy_all_option=True), NotImplementedError),
     ("MarketMaking", dict(reward_function="bogus"), ValueError),
     ("MarketMaking", dict(unwind_price="near_touch"), ValueError),
     ("Execution", dict(action_space="fixed_quants"), NotImplementedError),   # reference unpack error

@@ -194,6 +194,9 @@ MM_ACTION_VARIANTS = [
     dict(action_space="simple"), dict(action_space="simple", simple_nothing_action=False, n_ticks_offset=2),
     dict(action_space="simple", sell_buy_all_option=True, fixed_quant_value=2),
     dict(action_space="bobRL", bob_v0=2, fixed_action_setting=True, fixed_action=3),
+    dict(action_space="fixed_quants", sell_buy_all_option=True),            # 9-entry tables (mm_env.py:1018-1023)
+    dict(action_space="fixed_quants", sell_buy_all_option=True, fixed_quant_value=2, tenth_action="NA"),
+    dict(action_space="bobRL", bob_v0=2, sell_buy_all_option=True),          # the flag is not read by bobRL
 ]
 
 

@@ -166,6 +166,91 @@ def test_mm_action_messages_vs_numpy(changes):
     assert checked > 100
 
 
+# ------------------------------------------- MM fixed_quants / directional rows
+def fixed_quant_rows(t, w, rec, L, tid, action):
+    """_getActionMsgs_fixedQuant (mm_env.py:970-1118): [(type, side, qty, price)] x 2."""
+    tick, nO, M = w.tick_size, w.nOrders, L.n_msgs
+    asks = rec[L.off_asks:L.off_asks + 6 * nO].reshape(nO, 6)
+    bids = rec[L.off_bids:L.off_bids + 6 * nO].reshape(nO, 6)
+    inv = int(rec[L.agent_offsets[0] + 2])
+    if t.fixed_action_setting:
+        action = t.fixed_action
+    ba, bb = _masked_best(asks, bids, tid, w.maxint)
+    empty = ba == -1 or bb == -1
+    ba, bb = (ba // tick) * tick, (bb // tick) * tick
+    if empty:
+        ba, bb = int(rec[L.off_best_asks + 2 * (M - 1)]), int(rec[L.off_best_bids + 2 * (M - 1)])
+    fq = t.fixed_quant_value
+    if not t.sell_buy_all_option:
+        i = _gather(action, 10)
+        bo, ao = [0, 1, 2, 3, 4, 0, 2, 5, 1, 0][i], [0, 1, 2, 3, 4, 2, 0, 1, 5, 0][i]
+        bq = aq = [1] * 9 + [0]
+        bq, aq = bq[i] * fq, aq[i] * fq
+    else:
+        i = _gather(action, 9)
+        bo, ao = [10, 2, 4, -1, 0, 2, -20, 0, 0][i], [10, 2, 4, -1, 2, 0, 0, -20, 0][i]
+        bq = [1, 1, 1, 1, 1, 1, inv // fq, 0, 0][i] * fq
+        aq = [1, 1, 1, 1, 1, 1, 0, inv // fq, 0][i] * fq
+    if empty:
+        bq = aq = 0
+    hsp = max(F(F(ba - bb) / F(2)), F(F(tick) / F(2)))
+    hs = F(F(_fdiv(hsp, tick) + F(1)) * F(tick))
+    bp = _cvt(F(_fdiv(max(F(F(bb) - F(F(bo) * hs)), F(0)), tick) * F(tick)))
+    ap = _cvt(F(_fdiv(max(F(bp + tick), F(F(ba) + F(F(ao) * hs))), tick) * F(tick)))
+    rows = [(1, 1, bq, bp), (1, -1, aq, ap)]
+    liq = [(4, -1, int(F(t.auto_liquidate_alpha) * F(max(-inv, 0))), _cvt(F(F(ba) + F(hs * F(10))))),
+           (4, 1, int(F(t.auto_liquidate_alpha) * F(max(inv, 0))), _cvt(F(F(bb) - F(hs * F(10)))))]
+    if t.tenth_action == "MarketOrder" and action == 9:
+        rows = liq
+    if t.auto_liquidate_threshold != 0 and abs(inv) > t.auto_liquidate_threshold:
+        rows = liq
+    return rows
+
+
+def directional_rows(t, w, rec, L, action):
+    """_getActionMsgs_directional_trading (mm_env.py:1810-1865)."""
+    tick, M = w.tick_size, L.n_msgs
+    ba = int(rec[L.off_best_asks + 2 * (M - 1)]) // tick * tick
+    bb = int(rec[L.off_best_bids + 2 * (M - 1)]) // tick * tick
+    i = _gather(action, 3)
+    return [(1, 1, [0, 1, 0][i] * t.fixed_quant_value, ba), (1, -1, [0, 0, 1][i] * t.fixed_quant_value, bb)]
+
+
+@pytest.mark.parametrize("changes", [dict(), dict(tenth_action="NA"), dict(auto_liquidate_threshold=2),
+                                     dict(sell_buy_all_option=True), dict(sell_buy_all_option=True, fixed_quant_value=2),
+                                     dict(fixed_action_setting=True, fixed_action=7),
+                                     dict(action_space="directional_trading", fixed_quant_value=3)],
+                         ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()) or "metric")
+def test_mm_fixed_quant_and_directional_vs_numpy(changes):
+    cfg = variant(builtin_config("2_player_fq_fqc"), "MarketMaking", **changes)
+    w = cfg.world_config
+    if "day" not in _DAY:
+        _DAY["day"] = generate_day(n_msgs=20_000, seed=5, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    day = _DAY["day"]
+    win = make_windows(day, w)
+    c, L = pack_env_cfg(cfg, len(win.starts), day.msgs.shape[0], True)
+    init = O.init_states(c.lob, win, day.msgs, w, L.init_rec_words)
+    E = 12
+    keys = np.arange(2 * E, dtype=np.uint32).reshape(E, 2) + 5
+    st, _ = O.env_reset(c, keys, init)
+    mm = cfg.dict_of_agents_configs["MarketMaking"]
+    tid = w.trader_id_range_start
+    liq = 0
+    for k in range(8):
+        for e in range(E):
+            for act in range(-1, mm.n_actions + 1):
+                rows, _ = O.mm_action_msgs(c, 0, 0, st[e], act)
+                want = (directional_rows(mm, w, st[e], L, act) if mm.action_space == "directional_trading"
+                        else fixed_quant_rows(mm, w, st[e], L, tid, act))
+                got = [tuple(int(v) for v in r[:4]) for r in rows]
+                assert got == want, f"step {k} env {e} action {act}: oracle {got} numpy {want}"
+                liq += got[0][0] == 4
+        acts = O.sample_actions(c, keys + 7 * k)
+        st = O.env_step(c, keys + 7 * k, acts, day.msgs, init, st)[0]
+    if mm.action_space == "fixed_quants" and mm.tenth_action == "MarketOrder" and not mm.fixed_action_setting:
+        assert liq > 0
+
+
 # ------------------------------------------------------------ MM observations
 def mm_obs_numpy(t, w, rec, L, a_off):
     """_get_obs_basic (mm_env.py:2963-3000) / _get_obs_engineered (:3004-3154), normalize_obs
