@@ -9,10 +9,15 @@
   the unfused three-launch form is checked bit-exact against it in
   tests/test_gpu_env.py.
 
-Launches: K eager launches back to back on one stream (--graph-steps G > 0
-replays a captured HIP graph of G launches instead; it measures the same on
-MI355X, since a 116 us kernel hides the host launch cost).  roofline.kernel_ms
-is the HIP-event time of the timed region on the launch stream / K.
+Launches (default): the K timed steps are one MARLEnv.rollout_sampled call
+(hftlob_env_rollout_sampled, Speed_test's whole scan): the 4096 envs run as 2
+contiguous slices, each stepped by its own k_env_step launches on its own
+stream, so one slice's slowest envs overlap the other slice's next step
+instead of idling CUs at every step boundary (bit-exact with K full-batch
+launches, tests/test_gpu_env.py).  --slices 0: one full-batch
+hftlob_env_step_sampled launch per step (--graph-steps G > 0 replays a
+captured HIP graph of G such launches).  roofline.kernel_ms is the HIP-event
+time of the timed region on the caller's stream / K.
 
 Weak scaling: every rank (one process per GPU) steps its own 4096 envs on a
 replicated synthetic LOBSTER day; no collective on the data path (only the
@@ -84,6 +89,12 @@ def main():
     ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
                     help="rollout: one fused launch per step (key split + action sampling + step); "
                          "step: split_keys, sample_actions and env.step as three launches (SURVEY.md 8(d))")
+    ap.add_argument("--slices", type=int, default=2,
+                    help="rollout mode: env slices on streams of their own (MARLEnv.rollout_sampled, 1..4; 2 is fastest "
+                         "on MI355X, 4 collapses); "
+                         "0 = one full-batch hftlob_env_step_sampled launch per step")
+    ap.add_argument("--steps-per-call", type=int, default=0,
+                    help="rollout mode with --slices: env steps per rollout_sampled call (0 = all timed steps)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
@@ -123,9 +134,14 @@ def main():
 
     rng = [kbuf[0].reshape(1, 2).clone()]
 
-    def one_step():
+    sliced = args.mode == "rollout" and args.slices > 0
+    T = (args.steps_per_call if args.steps_per_call > 0 else max(args.steps, 1)) if sliced else 1
+
+    def one_step(n=1):
         k = nstep[0]
-        if args.mode == "rollout":
+        if sliced:
+            env.rollout_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params, n, n_slices=args.slices)
+        elif args.mode == "rollout":
             env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)
         else:  # Speed_test's three calls, each its own launch: split, Discrete.sample, env.step
             ks = split_keys(rng[0], E + 1)[0]
@@ -133,10 +149,15 @@ def main():
             env.step(sk, state, env.sample_actions(sk), params)
         nstep[0] = k + 1
 
-    for _ in range(args.warmup):
-        one_step()
+    def run(n_steps):  # n_steps env steps as launches of T steps (the last one shorter)
+        while n_steps > 0:
+            one_step(min(T, n_steps))
+            n_steps -= T
+
+    run(args.warmup)
     torch.cuda.synchronize()
-    G = args.graph_steps if args.graph_steps > 0 and args.graph_steps % 2 == 0 and args.mode == "rollout" else 0
+    G = (args.graph_steps if args.graph_steps > 0 and args.graph_steps % 2 == 0 and args.mode == "rollout"
+         and T == 1 else 0)
     graph = None
     if G:
         # G consecutive launches in one HIP graph; G is even, so the key ping-pong buffers line up
@@ -165,13 +186,15 @@ def main():
         for _ in range(args.steps // G):
             graph.replay()
         done = args.steps // G * G
-    for _ in range(args.steps - done):
-        one_step()
+    run(args.steps - done)
     ev1.record()
     torch.cuda.synchronize()
     D.barrier(R)
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps   # average k_env_step launch duration, HIP events
+    # HIP events on the launch stream bracket the timed region.  Full-batch launches: the
+    # average k_env_step duration.  Sliced: per batched step (each k_env_step launch then
+    # covers one slice; rocprof's per-launch average is ~the slice's share of it).
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     # (step mode: the three launches of one step together; rocprof splits them)
     elapsed = D.max_over_ranks(R, elapsed, device="cuda")
 
@@ -185,7 +208,9 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            t = json.load(f)
+        if t.get("hbm_bytes_per_env_step") is not None:   # per batched env step, like `achieved`
+            traffic = round(t["hbm_bytes_per_env_step"] * E)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         n_env_cpu, n_steps_cpu = 4096, 64       # one full episode (incl. auto-reset) of the metric workload
@@ -211,10 +236,14 @@ def main():
                                 f"auto-reset, Speed_test semantics") if args.config == CONFIG else
                                f"{args.config}.json, {env.num_msgs_per_step} msgs/step, auto-reset, Speed_test semantics",
                    "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)",
-                   "launch": f"hipGraph of {G} steps" if G else "eager", "mode": args.mode},
+                   "launch": (f"hipGraph of {G} steps" if G else
+                              (f"eager, {args.slices} env slices on their own streams (rollout_sampled, "
+                               f"{T} steps per call)" if sliced else "eager")),
+                   "mode": args.mode},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
-                     "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env},
+                     "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "slices": args.slices if sliced else 1,
+                     "bytes_per_env_step": per_env},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HFTLOB_ABI_VERSION 4
+#define HFTLOB_ABI_VERSION 5
 
 #define HFTLOB_OK            0
 #define HFTLOB_EINVAL      (-1)   /* bad config value / unsupported option */
@@ -266,6 +266,24 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, con
                             uint32_t* key_out, int32_t* actions_out, const int32_t* msg_data,
                             const int32_t* init_states, int32_t* state, const hftlob_step_out* out /*[host] struct*/,
                             void* stream);
+
+/* n_steps consecutive Speed_test rollout steps — replaces the whole
+ * jax.lax.scan of Speed_test.py:186-196 (`rollout`): the same results, bit for
+ * bit, as n_steps hftlob_env_step_sampled calls with key_out fed back as
+ * key_in.  The envs are cut into n_slices (1..4) contiguous slices: slice 0
+ * is stepped on `stream`, the others on library-owned HIP streams forked from
+ * / joined back to it with events (no host synchronisation), so one slice's
+ * slowest envs overlap the other slices' next steps.  per_step != 0: out->{obs,rewards,done_all,
+ * dones,info} and actions_out hold a leading [n_steps] dimension (step t at
+ * offset t * their per-step size); per_step == 0: each step overwrites them
+ * (the scan discards them).  key_out receives the master key after n_steps
+ * splits.  Calls for one device must not run concurrently from several host
+ * threads (the slice streams and key buffers are per device). */
+int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, int n_steps,
+                               const uint32_t* key_in, uint32_t* key_out, int32_t* actions_out,
+                               const int32_t* msg_data, const int32_t* init_states, int32_t* state,
+                               const hftlob_step_out* out /*[host] struct*/, int per_step, int n_slices,
+                               void* stream);
 
 /* Speed_test action sampling (Speed_test.py:166-177, gymnax Discrete.sample):
  * for env e with step key k_e,

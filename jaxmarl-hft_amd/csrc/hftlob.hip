@@ -1913,6 +1913,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
 //                (Speed_test.py:166-177), agent ag's in lane 32 + ag
 struct StepKeys {
     Key key, k1, key_reset;
+    Key next_master;   // rollout mode: split(master, n_env + 1)[0], the key the next step splits
     u32 shuffle_bits;  // lane l < A: random word of action row l
     i32 acts;          // lane 32 + ag: sampled action (rollout mode)
 };
@@ -1929,15 +1930,15 @@ DEV Key from_lane(Key v, int src) {  // per-lane gather v[src]
     return Key{(u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.a), (u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.b)};
 }
 template <bool MD>  // MD: the config may hold MultiDiscrete (fixed_prices) agent types
-DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* keys, const u32* master, u32* master_out) {
+DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* keys, const Key* master) {
     const bool part = c.prng_partitionable;
     const int l = lane_id(), nTy = c.n_types, A = c.n_action_msgs;
     Key key;
+    Key nm{0u, 0u};
     if (master) {  // lane 0: this env's key; lane 1: the carried master key
-        const Key mk{master[0], master[1]};
-        const Key v = split_key(mk, n_env + 1, l == 0 ? e + 1 : 0, part);
+        const Key v = split_key(*master, n_env + 1, l == 0 ? e + 1 : 0, part);
         key = lane_key(v);
-        if ((e == 0) & (l == 1)) { master_out[0] = v.a; master_out[1] = v.b; }
+        nm = Key{(u32)rdl((i32)v.a, 1), (u32)rdl((i32)v.b, 1)};
     } else {
         key = Key{keys[2 * e], keys[2 * e + 1]};
     }
@@ -1949,6 +1950,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     const Key L1 = split_key(key, l < 2 ? 2 : nTy, l < 2 ? l : l - 2, part);
     StepKeys o;
     o.key = key;
+    o.next_master = nm;
     o.k1 = Key{(u32)rdl((i32)L1.a, 0), (u32)rdl((i32)L1.b, 0)};
     o.key_reset = Key{(u32)rdl((i32)L1.a, 1), (u32)rdl((i32)L1.b, 1)};
     // L2: lane 0 sk = split(k1)[1]; agent lanes: split(sub_t, n_agents_t)[i]
@@ -1987,19 +1989,16 @@ DEV void fixed_time_mask(int4& x, int4& y, i32 t_end) {
 template <int S, int NFIX, bool RC>
 // RC: cancel_mode 2/3 (the random cancel fallback of the engine).
 // master != NULL: Speed_test rollout mode — the env's step key is
-// split(master, n_env + 1)[e + 1], actions are sampled here (hftlob_sample_actions)
-// and written to actions_io if it is not NULL; env 0 writes split(master)[0]
-// to master_out.  Otherwise keys / actions_io are the inputs.
-__global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
-                                                 const u32* __restrict__ master, u32* __restrict__ master_out,
-                                                 i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
-                                                 const i32* __restrict__ init_states, i32* __restrict__ state,
-                                                 float* __restrict__ obs_out, float* __restrict__ rew_out,
-                                                 u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
-                                                 i32* __restrict__ info_out) {
-    extern __shared__ __attribute__((aligned(16))) i32 lds[];
-    const int e = blockIdx.x;
-    if (e >= n_env) return;
+// split(*master, n_env + 1)[e + 1], actions are sampled here (hftlob_sample_actions)
+// and written to actions_io if it is not NULL; *master becomes split(*master)[0].
+// Otherwise keys / actions_io are the inputs.
+// key_n / ek: the env count of the step-key split and this env's index in it;
+// e: this env's record / output index
+DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u32* __restrict__ keys, Key* master,
+                      i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
+                      const i32* __restrict__ init_states, i32* __restrict__ state, float* __restrict__ obs_out,
+                      float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
+                      i32* __restrict__ info_out, i32* lds) {
     STAMP(t_start);
     const int l = lane_id();
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
@@ -2015,7 +2014,8 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
     fetch_side(fa, rec + c.off_asks, B.vs);
     fetch_side(fb, rec + c.off_bids, B.vs);
-    const StepKeys SK = step_keys<NFIX == 0>(c, n_env, e, keys, master, master_out);
+    const StepKeys SK = step_keys<NFIX == 0>(c, key_n, ek, keys, master);
+    if (master) *master = SK.next_master;
     const Key key_reset = SK.key_reset;
     if (RC) {  // the scan's key: k1, or split(k1)[0] after the shuffle split (marl_env.py:293-294,349-351)
         B.ek = c.shuffle_action_messages ? split_key(SK.k1, 2, 0, c.prng_partitionable) : SK.k1;
@@ -2365,6 +2365,29 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, co
     }
 }
 
+// One launch = one batched step.  Env slices: block e steps record e of the
+// (offset) buffers, and derives its Speed_test step key as env key_e0 + e of a
+// split over key_n envs (split(master, key_n + 1)[key_e0 + e + 1]); a full-batch
+// launch has key_e0 = 0, key_n = n_env.  Block 0 writes the carried master key
+// split(master, key_n + 1)[0] to master_out.
+template <int S, int NFIX, bool RC>
+__global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, int key_e0, int key_n,
+                                                 const u32* __restrict__ keys, const u32* __restrict__ master,
+                                                 u32* __restrict__ master_out, i32* __restrict__ actions_io,
+                                                 const i32* __restrict__ msg_data, const i32* __restrict__ init_states,
+                                                 i32* __restrict__ state, float* __restrict__ obs_out,
+                                                 float* __restrict__ rew_out, u8* __restrict__ done_all_out,
+                                                 u8* __restrict__ dones_out, i32* __restrict__ info_out) {
+    extern __shared__ __attribute__((aligned(16))) i32 lds[];
+    const int e = blockIdx.x;
+    if (e >= n_env) return;
+    Key mk{0u, 0u};
+    if (master) mk = Key{master[0], master[1]};
+    env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master ? &mk : nullptr, actions_io, msg_data, init_states,
+                              state, obs_out, rew_out, done_all_out, dones_out, info_out, lds);
+    if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
+}
+
 // ==================================================== K3/K4: PRNG kernels
 __global__ void k_sample_actions(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys, i32* __restrict__ actions) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2521,16 +2544,17 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
     return launch_status();
 }
 
-static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const uint32_t* key_in,
-                           uint32_t* key_out, int32_t* actions, const int32_t* msg_data, const int32_t* init_states,
-                           int32_t* state, const hftlob_step_out* out, void* stream) {
+static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int key_n, const uint32_t* keys,
+                           const uint32_t* key_in, uint32_t* key_out, int32_t* actions, const int32_t* msg_data,
+                           const int32_t* init_states, int32_t* state, const hftlob_step_out* out, void* stream) {
     if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
     const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
                             12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
-#define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, *cfg, n_env, keys, key_in, key_out, \
+#define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, keys, \
+                                               key_in, key_out, \
                                                actions, msg_data, init_states, state, out->obs, out->rewards, \
                                                out->done_all, out->dones, out->info)
     if (cfg->lob.cancel_mode >= 2) {  // random cancel fallback: general sizes only
@@ -2555,8 +2579,8 @@ int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, 
     if (n_env < 0) return fail(HFTLOB_ESHAPE, "negative n_env");
     if (n_env == 0) return HFTLOB_OK;
     if (!keys || !actions || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
-    return env_step_launch(cfg, n_env, keys, nullptr, nullptr, const_cast<int32_t*>(actions), msg_data, init_states,
-                           state, out, stream);
+    return env_step_launch(cfg, n_env, 0, n_env, keys, nullptr, nullptr, const_cast<int32_t*>(actions), msg_data,
+                           init_states, state, out, stream);
 }
 
 int hftlob_env_step_sampled(const hftlob_env_cfg* cfg, int n_env, const uint32_t* key_in, uint32_t* key_out,
@@ -2568,8 +2592,91 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg, int n_env, const uint32_t
     if (n_env == 0) return HFTLOB_OK;
     if (!key_in || !key_out || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
     if (key_in == key_out) return fail(HFTLOB_EINVAL, "key_in and key_out must be distinct buffers");
-    return env_step_launch(cfg, n_env, nullptr, key_in, key_out, actions_out, msg_data, init_states, state, out,
+    return env_step_launch(cfg, n_env, 0, n_env, nullptr, key_in, key_out, actions_out, msg_data, init_states, state, out,
                            stream);
+}
+
+// Rollout: the batch is cut into G contiguous env slices, each stepped on a
+// stream of its own (forked from / joined back to the caller's stream with
+// events).  A step's launch waits only for the same slice's previous step, so
+// the slow envs at the end of one slice's step overlap the other slices' next
+// steps instead of idling the CUs at every step boundary.  Every slice carries
+// its own copy of the master key chain in a private ping-pong pair.
+#define ROLLOUT_MAX_SLICES 4
+struct RolloutCtx {
+    bool ready = false;
+    hipStream_t s[ROLLOUT_MAX_SLICES];
+    hipEvent_t fork, join[ROLLOUT_MAX_SLICES];
+    uint32_t* keys = nullptr;  // [slice][2 ping-pong][2]
+};
+static RolloutCtx g_rollout[64];
+
+static int rollout_ctx(RolloutCtx** out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(HFTLOB_ELAUNCH, "hipGetDevice");
+    RolloutCtx& r = g_rollout[dev];
+    if (!r.ready) {
+        for (int g = 0; g < ROLLOUT_MAX_SLICES; ++g) {
+            if (hipStreamCreateWithFlags(&r.s[g], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&r.join[g], hipEventDisableTiming) != hipSuccess)
+                return fail(HFTLOB_ELAUNCH, "rollout stream/event creation");
+        }
+        if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&r.keys, sizeof(uint32_t) * 4 * ROLLOUT_MAX_SLICES) != hipSuccess)
+            return fail(HFTLOB_ELAUNCH, "rollout event / key buffer");
+        r.ready = true;
+    }
+    *out = &r;
+    return HFTLOB_OK;
+}
+
+int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int n_steps, const uint32_t* key_in,
+                               uint32_t* key_out, int32_t* actions_out, const int32_t* msg_data,
+                               const int32_t* init_states, int32_t* state, const hftlob_step_out* out, int per_step,
+                               int n_slices, void* stream) {
+    int rc = check_env(cfg);
+    if (rc) return rc;
+    if (n_env < 0 || n_steps < 0) return fail(HFTLOB_ESHAPE, "negative n_env / n_steps");
+    if (n_slices < 1 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 1..4");
+    if (n_env == 0 || n_steps == 0) return HFTLOB_OK;
+    if (!key_in || !key_out || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
+    if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
+    if (key_in == key_out) return fail(HFTLOB_EINVAL, "key_in and key_out must be distinct buffers");
+    RolloutCtx* R = nullptr;
+    if ((rc = rollout_ctx(&R))) return rc;
+    const int G = n_slices < n_env ? n_slices : n_env;
+    hipStream_t caller = (hipStream_t)stream;
+    if (G > 1) {
+        if (hipEventRecord(R->fork, caller) != hipSuccess) return fail(HFTLOB_ELAUNCH, "fork event");
+    }
+    const size_t na = (size_t)cfg->n_agents;
+    for (int g = 0; g < G; ++g) {
+        const int e0 = (int)((long)n_env * g / G), e1 = (int)((long)n_env * (g + 1) / G), ne = e1 - e0;
+        // slice 0 runs on the caller's stream (one hardware queue fewer: GPU_MAX_HW_QUEUES is 4)
+        hipStream_t st = g > 0 ? R->s[g] : caller;
+        if (g > 0 && hipStreamWaitEvent(st, R->fork, 0) != hipSuccess) return fail(HFTLOB_ELAUNCH, "fork wait");
+        uint32_t* kb = R->keys + 4 * g;  // this slice's ping-pong pair
+        for (int t = 0; t < n_steps; ++t) {
+            const size_t o = per_step ? (size_t)t * n_env + e0 : (size_t)e0;
+            hftlob_step_out so;
+            so.obs = out->obs + o * na * cfg->obs_stride;
+            so.rewards = out->rewards + o * na;
+            so.done_all = out->done_all + o;
+            so.dones = out->dones + o * na;
+            so.info = out->info ? out->info + o * cfg->info_words : nullptr;
+            const uint32_t* kin = t == 0 ? key_in : kb + 2 * ((t - 1) & 1);
+            uint32_t* kout = t == n_steps - 1 ? (g == 0 ? key_out : kb + 2 * (t & 1)) : kb + 2 * (t & 1);
+            int32_t* acts = actions_out ? actions_out + o * cfg->action_words : nullptr;
+            rc = env_step_launch(cfg, ne, e0, n_env, nullptr, kin, kout, acts, msg_data, init_states,
+                                 state + (size_t)e0 * cfg->rec_words, &so, st);
+            if (rc) return rc;
+        }
+    }
+    for (int g = 1; g < G; ++g) {  // join after every slice is enqueued (the caller's own slice 0 included)
+        if (hipEventRecord(R->join[g], R->s[g]) != hipSuccess || hipStreamWaitEvent(caller, R->join[g], 0) != hipSuccess)
+            return fail(HFTLOB_ELAUNCH, "join event");
+    }
+    return HFTLOB_OK;
 }
 
 int hftlob_sample_actions(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, int32_t* actions, void* stream) {

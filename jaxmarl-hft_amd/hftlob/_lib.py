@@ -12,9 +12,10 @@ import os
 from .layout import EnvCfg, LobCfg, StepOut
 
 LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
-           "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_sample_actions", "hftlob_split_keys")
+           "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_env_rollout_sampled", "hftlob_sample_actions",
+           "hftlob_split_keys")
 
 _lib = None
 
@@ -43,6 +44,9 @@ def lib() -> C.CDLL:
     L.hftlob_env_step.restype = i32
     L.hftlob_env_step_sampled.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp, vp, vp, vp, C.POINTER(StepOut), vp]
     L.hftlob_env_step_sampled.restype = i32
+    L.hftlob_env_rollout_sampled.argtypes = [C.POINTER(EnvCfg), i32, i32, vp, vp, vp, vp, vp, vp,
+                                             C.POINTER(StepOut), i32, i32, vp]
+    L.hftlob_env_rollout_sampled.restype = i32
     L.hftlob_sample_actions.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp]
     L.hftlob_sample_actions.restype = i32
     L.hftlob_split_keys.argtypes = [i32, i32, i32, vp, vp, vp]

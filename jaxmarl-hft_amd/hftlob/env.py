@@ -361,6 +361,53 @@ class MARLEnv:
             _lib.ptr(state.buf), C.byref(o["struct"]), _lib.stream_ptr()))
         return self._results(o, state, E)
 
+    def rollout_sampled(self, key_in: torch.Tensor, key_out: torch.Tensor, state: MultiAgentState,
+                        params: MultiAgentParams, n_steps: int, per_step: bool = False,
+                        actions_out: Optional[torch.Tensor] = None, n_slices: int = 2):
+        """Speed_test's whole ``rollout`` scan (Speed_test.py:186-196): bit for bit
+        ``n_steps`` calls of :meth:`step_sampled` with ``key_out`` fed back as ``key_in``,
+        enqueued on the current stream without host synchronisation.  The envs run as
+        ``n_slices`` contiguous slices on streams of their own, so one slice's slow envs
+        overlap the others' next steps.  ``key_out`` receives the master key after the
+        n_steps splits.
+        per_step=False: the outputs are the last step's (the scan discards them);
+        per_step=True: obs / rewards / dones (and ``actions_out``, int32
+        [n_steps, E, action_words] if given) carry a leading [n_steps] dimension
+        (the info dict, when enabled, is flattened to [n_steps * E, ...])."""
+        E = state.buf.shape[0]
+        if n_steps < 1:
+            raise ValueError("n_steps must be >= 1")
+        if per_step:
+            L, dev, T = self.layout, self.device, n_steps
+            o = {"obs": torch.empty((T, E, self.num_agents, L.obs_stride), dtype=torch.float32, device=dev),
+                 "rewards": torch.empty((T, E, self.num_agents), dtype=torch.float32, device=dev),
+                 "done_all": torch.empty((T, E), dtype=torch.bool, device=dev),
+                 "dones": torch.empty((T, E, self.num_agents), dtype=torch.bool, device=dev),
+                 "info": torch.empty((T, E, L.info_words), dtype=torch.int32, device=dev) if self.return_info else None}
+            o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
+                                  _lib.ptr(o["dones"]), _lib.ptr(o["info"]) if o["info"] is not None else None)
+            shape = (n_steps, E, self.action_words)
+        else:
+            o = self._outputs(E)
+            shape = (E, self.action_words)
+        if actions_out is not None and (tuple(actions_out.shape) != shape or actions_out.dtype != torch.int32):
+            raise ValueError(f"actions_out must be int32 {list(shape)}")
+        _lib.check(_lib.lib().hftlob_env_rollout_sampled(
+            C.byref(self.cfg_c), E, n_steps, _lib.ptr(key_in), _lib.ptr(key_out), _lib.ptr(actions_out),
+            _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
+            _lib.ptr(state.buf), C.byref(o["struct"]), int(per_step), int(n_slices), _lib.stream_ptr()))
+        if not per_step:
+            return self._results(o, state, E)
+        T = n_steps
+        flat = {k: (v.reshape((T * E,) + tuple(v.shape[2:])) if isinstance(v, torch.Tensor) else v)
+                for k, v in o.items()}
+        obs, _, rewards, dones, info = self._results(flat, state, T * E)
+        unf = lambda x: x.reshape((T, E) + tuple(x.shape[1:]))  # noqa: E731
+        obs = [unf(x) for x in obs]
+        rewards = [unf(x) for x in rewards]
+        dones = {"__all__": unf(dones["__all__"]), "agents": [unf(x) for x in dones["agents"]]}
+        return obs, state, rewards, dones, info
+
     def _results(self, o, state, E):
         self.last_info_words = o["info"]  # raw info record of the last step (int32 [E, info_words]) or None
         obs = self._split_types(o["obs"], True)

@@ -286,6 +286,76 @@ def test_step_sampled_equals_split_sample_step(name, part, exe):
         assert (da1 == d2["__all__"]).all()
 
 
+@pytest.mark.parametrize("name,part,exe,T,per_step,G", [("2_player_fq_fqc", True, None, 70, False, 4),
+                                                          ("2_player_fq_fqc", True, None, 7, True, 3),
+                                                          ("2_player_fq_fqc", True, None, 5, True, 1),
+                                                          ("3_player_fq_fqc_dir", False, None, 13, True, 2),
+                                                          ("exec_debug_fixed_quants_complex", False, 2, 9, True, 4)])
+def test_rollout_sampled_equals_step_sampled(name, part, exe, T, per_step, G):
+    """hftlob_env_rollout_sampled (T steps over G env slices on their own streams) == T
+    hftlob_env_step_sampled launches: state, carried key, and (per_step) every step's
+    actions / obs / rewards / dones, bit for bit; the rollout crosses an auto-reset."""
+    cfg = builtin_config(name)
+    if exe:
+        cfg = variant(cfg, "Execution", action_space="fixed_prices", n_actions=exe, fixed_quant_value=11)
+    w = cfg.world_config
+    env = MARLEnv(None, cfg, data=_day(w, 2_000_000), prng_partitionable=part)
+    params = env.default_params
+    E = 40
+    keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
+    _, s1 = env.reset(keys, params)
+    s2 = s1.clone(env)
+    k0 = torch.tensor([3, 9], dtype=torch.int32, device="cuda")
+    # prefix of steps so the T-step launch crosses the episode end
+    pre = 60 if T < 70 else 0
+    kbuf = [k0.clone(), torch.empty(2, dtype=torch.int32, device="cuda")]
+    for k in range(pre):
+        env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], s1, params)
+    s2 = s1.clone(env)
+    kin = kbuf[pre % 2].clone()
+    ref_acts, ref_obs, ref_rew, ref_done = [], [], [], []
+    acts_out = torch.empty((E, env.action_words), dtype=torch.int32, device="cuda")
+    for k in range(pre, pre + T):
+        o1, s1, r1, d1, _ = env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], s1, params, acts_out)
+        ref_acts.append(acts_out.clone())
+        ref_obs.append([x.clone() for x in o1])
+        ref_rew.append([x.clone() for x in r1])
+        ref_done.append(d1["__all__"].clone())
+    kout = torch.empty(2, dtype=torch.int32, device="cuda")
+    shape = (T, E, env.action_words) if per_step else (E, env.action_words)
+    acts2 = torch.empty(shape, dtype=torch.int32, device="cuda")
+    o2, s2, r2, d2, _ = env.rollout_sampled(kin, kout, s2, params, T, per_step=per_step, actions_out=acts2,
+                                            n_slices=G)
+    assert (kout == kbuf[(pre + T) % 2]).all(), "carried key"
+    assert (s1.buf == s2.buf).all(), "state after the rollout"
+    steps = range(T) if per_step else [T - 1]
+    for t in steps:
+        pick = (lambda x: x[t]) if per_step else (lambda x: x)  # noqa: E731
+        assert (pick(acts2) == ref_acts[t]).all(), f"step {t}: actions"
+        assert all((pick(a) == b).all() for a, b in zip(o2, ref_obs[t])), f"step {t}: obs"
+        assert all((pick(a) == b).all() for a, b in zip(r2, ref_rew[t])), f"step {t}: rewards"
+        assert (pick(d2["__all__"]) == ref_done[t]).all(), f"step {t}: done"
+
+
+def test_rollout_sampled_random_cancel():
+    """the cancel_mode 2/3 instantiation of the multi-step kernel: a 66-step launch == 66 launches"""
+    cfg = builtin_config("2_player_fq_fqc")
+    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, cancel_mode=3))
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
+    params = env.default_params
+    E = 24
+    keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
+    _, s1 = env.reset(keys, params)
+    s2 = s1.clone(env)
+    kbuf = [torch.tensor([1, 2], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
+    kin = kbuf[0].clone()
+    for k in range(66):
+        env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], s1, params)
+    kout = torch.empty(2, dtype=torch.int32, device="cuda")
+    env.rollout_sampled(kin, kout, s2, params, 66, n_slices=3)
+    assert (kout == kbuf[0]).all() and (s1.buf == s2.buf).all()
+
+
 @pytest.mark.parametrize("name,agents,changes", [
     ("2_player_fq_fqc", [3, 2], None),                     # several agents of each type
     ("3_player_fq_fqc_dir", [2, 2, 3], None),
