@@ -80,6 +80,19 @@ def test_error_null_and_shape(L):
     assert L.hftlob_env_step_sampled(C.byref(c), 4, k, None, None, k, k, k, C.byref(out), None) == -2
     assert L.hftlob_env_step_sampled(C.byref(c), 4, k, k, None, k, k, k, C.byref(out), None) == -1  # key_in == key_out
     assert L.hftlob_sample_actions(None, 4, None, None, None) == -2
+    # hftlob_env_rollout_sampled: argument checks run before any HIP call
+    R = L.hftlob_env_rollout_sampled
+    assert R(None, 4, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -2            # null cfg
+    assert R(C.byref(c), -1, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3     # negative n_env
+    assert R(C.byref(c), 4, -1, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3     # negative n_steps
+    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(out), 0, 0, None) == -1      # n_slices 0
+    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(out), 0, 5, None) == -1      # n_slices > 4
+    assert R(C.byref(c), 0, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0       # empty batch
+    assert R(C.byref(c), 4, 0, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0       # no steps
+    assert R(C.byref(c), 4, 8, k, None, None, k, k, k, C.byref(out), 0, 2, None) == -2   # null key_out
+    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -2      # null outputs
+    full = StepOut(k, k, k, k, None)
+    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(full), 0, 2, None) == -1     # key_in == key_out
 
 
 @pytest.mark.parametrize("field,value,code", [("cancel_mode", 4, -1), ("type_4_interpretation", 3, -1),
