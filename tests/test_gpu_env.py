@@ -337,6 +337,41 @@ def test_rollout_sampled_equals_step_sampled(name, part, exe, T, per_step, G):
         assert (pick(d2["__all__"]) == ref_done[t]).all(), f"step {t}: done"
 
 
+def test_rollout_sampled_graph_capture():
+    """a 2-slice rollout_sampled captured in a HIP graph (the slice stream joins the capture through
+    the fork / join events) replays to the same state and carried key as the eager call"""
+    cfg = builtin_config("2_player_fq_fqc")
+    # return_info=False as in the learner and the bench: the info dict's host-side index lists copy to the
+    # device, which a capture does not allow
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000), persistent_outputs=True, return_info=False)
+    params = env.default_params
+    E, T = 64, 10
+    keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
+    _, s1 = env.reset(keys, params)
+    s2 = s1.clone(env)
+    s_start = s1.clone(env)
+    k0 = torch.tensor([4, 2], dtype=torch.int32, device="cuda")
+    kin, kout = k0.clone(), torch.empty(2, dtype=torch.int32, device="cuda")
+    env.rollout_sampled(kin, kout, s1, params, T, n_slices=2)
+    torch.cuda.synchronize()
+    gin, gout = torch.empty(2, dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):                      # warm-up outside the capture (library streams, events)
+        gin.copy_(k0)
+        env.rollout_sampled(gin, gout, s2, params, T, n_slices=2)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        env.rollout_sampled(gin, gout, s2, params, T, n_slices=2)
+    s2.buf.copy_(s_start.buf)
+    gin.copy_(k0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert (gout == kout).all() and (s2.buf == s1.buf).all()
+
+
 def test_rollout_sampled_random_cancel():
     """the cancel_mode 2/3 instantiation of the multi-step kernel: a 66-step launch == 66 launches"""
     cfg = builtin_config("2_player_fq_fqc")
