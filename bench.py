@@ -89,9 +89,9 @@ def main():
     ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
                     help="rollout: one fused launch per step (key split + action sampling + step); "
                          "step: split_keys, sample_actions and env.step as three launches (SURVEY.md 8(d))")
-    ap.add_argument("--slices", type=int, default=2,
-                    help="rollout mode: env slices on streams of their own (MARLEnv.rollout_sampled, 1..4; 2 is fastest "
-                         "on MI355X, 4 collapses); "
+    ap.add_argument("--slices", type=int, default=-1,
+                    help="rollout mode: env slices on streams of their own (MARLEnv.rollout_sampled, 1..4; "
+                         "-1 = MARLEnv.default_slices: 2 from 2048 envs up, else 1; 4 collapses on MI355X); "
                          "0 = one full-batch hftlob_env_step_sampled launch per step")
     ap.add_argument("--steps-per-call", type=int, default=0,
                     help="rollout mode with --slices: env steps per rollout_sampled call (0 = all timed steps)")
@@ -134,6 +134,8 @@ def main():
 
     rng = [kbuf[0].reshape(1, 2).clone()]
 
+    if args.slices < 0:
+        args.slices = MARLEnv.default_slices(E)
     sliced = args.mode == "rollout" and args.slices > 0
     T = (args.steps_per_call if args.steps_per_call > 0 else max(args.steps, 1)) if sliced else 1
 
