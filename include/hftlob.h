@@ -277,8 +277,11 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, con
  * dones,info} and actions_out hold a leading [n_steps] dimension (step t at
  * offset t * their per-step size); per_step == 0: each step overwrites them
  * (the scan discards them).  key_out receives the master key after n_steps
- * splits.  Calls for one device must not run concurrently from several host
- * threads (the slice streams and key buffers are per device). */
+ * splits.  The slice streams, events and key buffers are per device: calls
+ * for one device must be issued from one host thread at a time and on one
+ * caller stream (successive calls on that stream are ordered by the fork /
+ * join events; calls overlapping on different caller streams would share the
+ * slice key buffers). */
 int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, int n_steps,
                                const uint32_t* key_in, uint32_t* key_out, int32_t* actions_out,
                                const int32_t* msg_data, const int32_t* init_states, int32_t* state,

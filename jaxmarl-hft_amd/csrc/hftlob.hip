@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
+#include <mutex>
 #include <limits.h>
 
 #include "../../include/hftlob.h"
@@ -2611,9 +2612,12 @@ struct RolloutCtx {
 };
 static RolloutCtx g_rollout[64];
 
+static std::mutex g_rollout_mu;
+
 static int rollout_ctx(RolloutCtx** out) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(HFTLOB_ELAUNCH, "hipGetDevice");
+    std::lock_guard<std::mutex> lock(g_rollout_mu);  // one-time creation of the device's streams / buffers
     RolloutCtx& r = g_rollout[dev];
     if (!r.ready) {
         for (int g = 0; g < ROLLOUT_MAX_SLICES; ++g) {
