@@ -289,6 +289,16 @@ class MARLEnv:
             k += n * wd
         return out
 
+    def _info_index(self, a: int, n_t: int, k: int) -> torch.Tensor:
+        """device index of info word k for agents a..a+n_t-1, cached: no host copy per step
+        (so the info dict can be built inside a HIP graph capture)"""
+        cache = self.__dict__.setdefault("_info_idx", {})
+        key = (a, n_t, k)
+        if key not in cache:
+            cache[key] = torch.tensor([INFO_WORLD_WORDS + (a + i) * INFO_AGENT_WORDS + k for i in range(n_t)],
+                                      dtype=torch.long, device=self.device)
+        return cache[key]
+
     def _info(self, o, E):
         if o["info"] is None:
             return {}
@@ -306,8 +316,7 @@ class MARLEnv:
             fields = INFO_MM if self.layout.agent_kinds[a] == AGENT_MM else INFO_EXE
             d = {}
             for k, (n, isf) in enumerate(fields):
-                idx = [INFO_WORLD_WORDS + (a + i) * INFO_AGENT_WORDS + k for i in range(n_t)]
-                d[n] = (f if isf else info)[:, idx]
+                d[n] = (f if isf else info).index_select(1, self._info_index(a, n_t, k))
             agents.append(d)
             a += n_t
         return {"world": world, "agents": agents}

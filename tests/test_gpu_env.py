@@ -341,9 +341,7 @@ def test_rollout_sampled_graph_capture():
     """a 2-slice rollout_sampled captured in a HIP graph (the slice stream joins the capture through
     the fork / join events) replays to the same state and carried key as the eager call"""
     cfg = builtin_config("2_player_fq_fqc")
-    # return_info=False as in the learner and the bench: the info dict's host-side index lists copy to the
-    # device, which a capture does not allow
-    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000), persistent_outputs=True, return_info=False)
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000), persistent_outputs=True)
     params = env.default_params
     E, T = 64, 10
     keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
