@@ -134,8 +134,10 @@ def main():
 
     rng = [kbuf[0].reshape(1, 2).clone()]
 
-    if args.slices < 0:
-        args.slices = MARLEnv.default_slices(E)
+    if args.slices < 0:   # --graph-steps replays captured full-batch launches: unsliced
+        args.slices = 0 if args.graph_steps > 0 else MARLEnv.default_slices(E)
+    if args.graph_steps > 0 and args.slices > 0:
+        raise SystemExit("--graph-steps needs --slices 0 (it captures full-batch launches)")
     sliced = args.mode == "rollout" and args.slices > 0
     T = (args.steps_per_call if args.steps_per_call > 0 else max(args.steps, 1)) if sliced else 1
 
