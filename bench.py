@@ -2,44 +2,105 @@
 2_player_fq_fqc.json), NUM_ENVS=4096 per GPU, Speed_test semantics
 (gymnax_exchange/jaxen/Speed_test.py:140-224):
 
-  per step:  rng, *step_keys = split(rng, NUM_ENVS + 1)
-             actions = per-type randint from split(step_key, n_types)
-             env.step(step_key, state, actions, params)
-  all three in ONE HIP launch (MARLEnv.step_sampled -> hftlob_env_step_sampled);
-  the unfused three-launch form is checked bit-exact against it in
-  tests/test_gpu_env.py.
+  master_key, *reset_keys = split(PRNGKey(0), NUM_ENVS + 1);  state0 = reset(reset_keys)
+  rollout(state0, master_key, K):  per step  rng, *step_keys = split(rng, NUM_ENVS + 1)
+                                             actions = per-type randint from split(step_key, n_types)
+                                             env.step(step_key, state, actions, params)
+  a compile run (here: W warm-up steps), then the timed run of K steps from the same
+  state0 and master_key.
 
-Launches (default): the K timed steps are one MARLEnv.rollout_sampled call
-(hftlob_env_rollout_sampled, Speed_test's whole scan): the 4096 envs run as 2
-contiguous slices, each stepped by its own k_env_step launches on its own
-stream, so one slice's slowest envs overlap the other slice's next step
-instead of idling CUs at every step boundary (bit-exact with K full-batch
-launches, tests/test_gpu_env.py).  --slices 0: one full-batch
-hftlob_env_step_sampled launch per step (--graph-steps G > 0 replays a
-captured HIP graph of G such launches).  roofline.kernel_ms is the HIP-event
-time of the timed region on the caller's stream / K.
+The K timed steps are one MARLEnv.rollout_sampled call (hftlob_env_rollout_sampled,
+Speed_test's whole scan): split + sample + step fused per launch, the envs as 2 contiguous
+slices on their own streams so one slice's slowest envs overlap the other slice's next step
+(bit-exact with K full-batch launches, tests/test_gpu_env.py).  --mode step: Speed_test's three
+calls (split_keys, sample_actions, env.step) as three launches per step.
 
-Weak scaling: every rank (one process per GPU) steps its own 4096 envs on a
-replicated synthetic LOBSTER day; no collective on the data path (only the
-timing barrier / max-over-ranks).  Prints ONE JSON line on rank 0.
+Multi-GPU (weak scaling, one process per GPU): `--gpus N` launches N ranks itself when it is
+not already running under torchrun; rank r owns envs [r*E, (r+1)*E) of ONE Speed_test rollout
+over N*E envs (reset keys split(PRNGKey(0), N*E+1)[1+r*E : 1+(r+1)*E], step keys
+split(master, N*E+1)[1 + r*E + e]: the reference's pmap layout, ippo_rnn_JAXMARL_pmap.py:292-332).
+Day and init-state table are replicated; no collective on the data path (RCCL only for the
+timing barrier and the max over ranks).  --dry-run stops before the GPU (gloo) and prints the
+rank layout.  Rank 0 prints ONE JSON line.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "jaxmarl-hft_amd"))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
 NUM_ENVS = 4096
 CONFIG = "2_player_fq_fqc"
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+N_CU, CLOCK_HZ = 256, 2.4e9    # MI355X CUs, max engine clock (MI355X_MICROARCH.md)
+CPU_STEPS = 64                 # CPU baseline / parity: one full episode (incl. the auto-reset)
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs = ranks (one process per GPU)")
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--envs", type=int, default=NUM_ENVS, help="envs per GPU")
+    ap.add_argument("--n-msgs", type=int, default=400_000, help="synthetic day length (messages)")
+    ap.add_argument("--mid", type=int, default=2_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default=CONFIG, help="builtin env config (the metric: 2_player_fq_fqc)")
+    ap.add_argument("--agents", default=None, help="number_of_agents_per_type override, e.g. 5,5 (Speed_test sweep)")
+    ap.add_argument("--n-data-msg", type=int, default=None, help="n_data_msg_per_step override (Speed_test: 100, 1)")
+    ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
+                    help="rollout: one fused launch per step (key split + action sampling + step); "
+                         "step: split_keys, sample_actions and env.step as three launches (SURVEY.md 8(d))")
+    ap.add_argument("--slices", type=int, default=-1,
+                    help="rollout mode: env slices on streams of their own (1..4; -1 = MARLEnv.default_slices)")
+    ap.add_argument("--steps-per-call", type=int, default=0,
+                    help="rollout mode: env steps per rollout_sampled call (0 = all timed steps in one call)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the cores this process "
+                                                               "may use, capped by OMP_NUM_THREADS)")
+    ap.add_argument("--dry-run", action="store_true", help="rank layout only: no GPU (gloo), one JSON line")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args) -> int:
+    """`--gpus N` outside torchrun: start N rank processes (this process never touches the GPU)
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, wait for all of them, and
+    return the first failing exit code (the others are then terminated)."""
+    n, port = args.gpus, _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ------------------------------------------------------------------ helpers
 def algorithmic_bytes_per_env_step(env) -> int:
     """HBM bytes one env-step must move, from the live layout."""
     L, cfg = env.layout, env.multi_agent_config
@@ -53,176 +114,225 @@ def algorithmic_bytes_per_env_step(env) -> int:
     return reads + writes + reset
 
 
-def cpu_baseline(env, day, n_envs, n_steps, threads):
-    """The CPU oracle (plain-C restatement of the reference, OpenMP over envs), timed on this host."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _profile(name):
+    p = os.path.join(ROOT, "profiles", name)
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def compare_states(env, cpu, gpu) -> str:
+    """Integer words of the record bit-exact, float words within 1e-5."""
+    import numpy as np
+    L = env.layout
+    fw = [L.off_world + 3, L.off_world + 4]
+    for k, off in zip(L.agent_kinds, L.agent_offsets):
+        fw += [off + 3, off + 4] if k == 0 else [off + j for j in (0, 4, 5, 6, 7, 8, 9, 10, 11, 12)]
+    mask = np.ones(cpu.shape[1], bool)
+    mask[fw] = False
+    bad = int(((cpu != gpu) & mask[None, :]).sum())
+    if bad:
+        raise AssertionError(f"cpu_baseline parity: {bad} integer state words differ between the CPU oracle and "
+                             "the GPU rollout")
+    if not np.allclose(cpu[:, fw].view(np.float32), gpu[:, fw].view(np.float32), rtol=1e-5, atol=1e-5,
+                       equal_nan=True):
+        raise AssertionError("cpu_baseline parity: float state words differ beyond 1e-5")
+    return (f"end state of the {cpu.shape[0]}-env x {CPU_STEPS}-step rollout == the GPU's: "
+            f"{int(mask.sum())} int words/env bit-exact, {len(fw)} float words/env within 1e-5")
+
+
+def cpu_baseline(env, day, state0, master0, n_threads):
+    """The plain-C restatement (oracle/oracle.c, test infrastructure) built -O3 -march=native on
+    this host, its Speed_test rollout loop in C, timed on this host's cores: the metric workload
+    (4096 envs x one 64-step episode) on n_threads cores and on 1 core.  Returns the line's
+    object and the end state (for the parity check against the GPU)."""
+    import numpy as np
     sys.path.insert(0, ROOT)
     from oracle import pyoracle as O
-    threads = O.set_threads(threads)
-    c = env.cfg_c
-    init = env._init_states.cpu().numpy()
-    rng = np.arange(2, dtype=np.uint32)
-    keys = O.split_keys(rng[None], n_envs + 1)[0][1:]
-    state, _ = O.env_reset(c, keys, init)
+    model = _cpu_model()
+    tag = hashlib.sha1((model + open(os.path.join(ROOT, "oracle", "oracle.c")).read()).encode()).hexdigest()[:12]
+    L = O.native_lib(f"/tmp/hftlob_oracle_native_{tag}.so")
+    c, msgs, init = env.cfg_c, day.msgs, env._init_states.cpu().numpy()
+    st0 = state0.cpu().numpy()
+    m0 = master0.cpu().numpy().view(np.uint32)
+    E = st0.shape[0]
+    thr = L.oracle_set_threads(n_threads)
     t0 = time.perf_counter()
-    master = np.array([0, 1], np.uint32)
-    for _ in range(n_steps):
-        ks = O.split_keys(master[None], n_envs + 1)[0]
-        master, step_keys = ks[0].copy(), ks[1:].copy()
-        acts = O.sample_actions(c, step_keys)
-        state, *_ = O.env_step(c, step_keys, acts, day.msgs, init, state, with_info=False)
-    dt = time.perf_counter() - t0
-    return n_envs * n_steps / dt, threads
+    st, _ = O.rollout_sampled(c, m0, msgs, init, st0, CPU_STEPS, L=L)
+    v = E * CPU_STEPS / (time.perf_counter() - t0)
+    L.oracle_set_threads(1)
+    t0 = time.perf_counter()
+    st1, _ = O.rollout_sampled(c, m0, msgs, init, st0, CPU_STEPS, L=L)
+    v1 = E * CPU_STEPS / (time.perf_counter() - t0)
+    L.oracle_set_threads(thr)
+    if not (st1 == st).all():
+        raise AssertionError("cpu_baseline: 1-thread and multi-thread CPU rollouts differ")
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"value": round(v, 1), "unit": "env steps/s", "cores": thr, "kind": "port",
+            "sample": (f"{E} envs x {CPU_STEPS} steps (one episode incl. auto-reset) of the metric config/day/seeds, "
+                       "Speed_test rollout loop in C (oracle/oracle.c oracle_rollout_sampled), "
+                       f"gcc -O3 -march=native, OpenMP {thr} threads"),
+            "single_core_value": round(v1, 1), "single_core_sample": f"the same {E} x {CPU_STEPS} workload, 1 thread",
+            "cpu_model": model, "nproc": os.cpu_count(), "affinity_cores": aff}, st
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128)
-    ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--envs", type=int, default=NUM_ENVS, help="envs per GPU")
-    ap.add_argument("--n-msgs", type=int, default=400_000, help="synthetic day length (messages)")
-    ap.add_argument("--mid", type=int, default=2_000_000)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--graph-steps", type=int, default=0,
-                    help="steps per captured HIP graph in the timed region (even; 0 = eager launches)")
-    ap.add_argument("--config", default=CONFIG, help="builtin env config (the metric: 2_player_fq_fqc)")
-    ap.add_argument("--mode", choices=("rollout", "step"), default="rollout",
-                    help="rollout: one fused launch per step (key split + action sampling + step); "
-                         "step: split_keys, sample_actions and env.step as three launches (SURVEY.md 8(d))")
-    ap.add_argument("--slices", type=int, default=-1,
-                    help="rollout mode: env slices on streams of their own (MARLEnv.rollout_sampled, 1..4; "
-                         "-1 = MARLEnv.default_slices: 2 from 2048 envs up, else 1; 4 collapses on MI355X); "
-                         "0 = one full-batch hftlob_env_step_sampled launch per step")
-    ap.add_argument("--steps-per-call", type=int, default=0,
-                    help="rollout mode with --slices: env steps per rollout_sampled call (0 = all timed steps)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    args = ap.parse_args()
+# ------------------------------------------------------------------ rank body
+def dry_run(args):
+    """Rank layout without the GPU: gloo process group, each rank's env block and key rows."""
+    from hftlob import dist as D
+    R = D.init_from_env("gloo")
+    E = args.envs
+    a, b = D.env_slice(R.rank, E)
+    mine = {"rank": R.rank, "envs": [a, b], "reset_key_rows": [1 + a, 1 + b], "key_e0": a, "key_n": R.world * E}
+    gathered = [mine]
+    if R.dist is not None:
+        gathered = [None] * R.world
+        R.dist.all_gather_object(gathered, mine)
+    if R.rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": R.world, "num_envs_per_gpu": E,
+                          "num_envs_total": R.world * E, "ranks": sorted(gathered, key=lambda g: g["rank"])}))
+    D.finalize(R)
 
+
+def main(argv=None):
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args)
+    if args.dry_run:
+        return dry_run(args)
+    import numpy as np
+    import torch
     from hftlob import dist as D
     R = D.init_from_env("nccl")
     world, rank, local = R.world, R.rank, R.local
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
 
+    import dataclasses
     from hftlob.config_io import builtin_config
-    from hftlob.data.synthetic import generate_day
+    from hftlob.data.synthetic import LobsterDay, generate_day
     from hftlob.env import MARLEnv, split_keys
-    from hftlob import _lib
 
     cfg = builtin_config(args.config)
+    if args.agents:
+        cfg = dataclasses.replace(cfg, number_of_agents_per_type=[int(x) for x in args.agents.split(",")])
+    if args.n_data_msg:
+        cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config,
+                                                                        n_data_msg_per_step=args.n_data_msg))
     w = cfg.world_config
     snap = w.n_data_msg_per_step * w.start_resolution
     cache = f"/tmp/hftlob_day_{args.n_msgs}_{args.mid}_{snap}.npz"
-    if rank == 0 and not os.path.exists(cache):
+    if local == 0 and not os.path.exists(cache):
         d = generate_day(n_msgs=args.n_msgs, mid=args.mid, snap_every=snap)
-        np.savez(cache + ".tmp.npz", msgs=d.msgs, books=d.books, snap_idx=d.snap_idx, tick=d.tick_size)
-        os.replace(cache + ".tmp.npz", cache)
+        np.savez(cache + f".{os.getpid()}.npz", msgs=d.msgs, books=d.books, snap_idx=d.snap_idx, tick=d.tick_size)
+        os.replace(cache + f".{os.getpid()}.npz", cache)
     D.barrier(R)
-    from hftlob.data.synthetic import LobsterDay
     z = np.load(cache)
     day = LobsterDay(msgs=z["msgs"], books=z["books"], snap_idx=z["snap_idx"], tick_size=int(z["tick"]))
 
     E = args.envs
-    env = MARLEnv(None, cfg, data=day, device=f"cuda:{local}", return_info=False, persistent_outputs=True)
+    env = MARLEnv(None, cfg, data=day, device=dev, return_info=False, persistent_outputs=True)
     params = env.default_params
-    # global key split, then this rank's slice (reference pmap layout: contiguous env blocks)
-    master = torch.tensor([[0, 0]], dtype=torch.int32, device="cuda")
-    all_keys = split_keys(master, world * E + 1)[0]
-    keys0 = D.rank_keys(all_keys, rank, E).contiguous()
-    _, state = env.reset(keys0, params)
-    kbuf = [torch.tensor([0, 1 + rank], dtype=torch.int32, device="cuda"), torch.empty(2, dtype=torch.int32, device="cuda")]
+    # Speed_test: master_key, *reset_keys = split(PRNGKey(0), NUM_ENVS + 1), NUM_ENVS = world * E
+    all_keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device=dev), world * E + 1)[0]
+    master0 = all_keys[0].clone()
+    _, state = env.reset(D.rank_keys(all_keys, rank, E).contiguous(), params)
+    state0 = state.buf.clone()
+    key_e0, key_n = rank * E, world * E
+    if args.slices < 0:
+        args.slices = MARLEnv.default_slices(E)
+    if args.mode == "rollout":
+        env.prepare_rollout(args.slices)
+    T = (args.steps_per_call if args.steps_per_call > 0 else max(args.steps, 1)) if args.mode == "rollout" else 1
+    kbuf = [master0.clone(), torch.empty(2, dtype=torch.int32, device=dev)]
     nstep = [0]
 
-    rng = [kbuf[0].reshape(1, 2).clone()]
-
-    if args.slices < 0:   # --graph-steps replays captured full-batch launches: unsliced
-        args.slices = 0 if args.graph_steps > 0 else MARLEnv.default_slices(E)
-    if args.graph_steps > 0 and args.slices > 0:
-        raise SystemExit("--graph-steps needs --slices 0 (it captures full-batch launches)")
-    sliced = args.mode == "rollout" and args.slices > 0
-    T = (args.steps_per_call if args.steps_per_call > 0 else max(args.steps, 1)) if sliced else 1
-
-    def one_step(n=1):
-        k = nstep[0]
-        if sliced:
-            env.rollout_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params, n, n_slices=args.slices)
-        elif args.mode == "rollout":
-            env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)
-        else:  # Speed_test's three calls, each its own launch: split, Discrete.sample, env.step
-            ks = split_keys(rng[0], E + 1)[0]
-            rng[0], sk = ks[0:1], ks[1:]
-            env.step(sk, state, env.sample_actions(sk), params)
-        nstep[0] = k + 1
-
-    def run(n_steps):  # n_steps env steps as launches of T steps (the last one shorter)
+    def run(n_steps):  # n_steps env steps continuing the rollout from (state, kbuf)
         while n_steps > 0:
-            one_step(min(T, n_steps))
-            n_steps -= T
+            n, k = min(T, n_steps), nstep[0]
+            if args.mode == "rollout":
+                env.rollout_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params, n, n_slices=args.slices,
+                                    key_e0=key_e0, key_n=key_n)
+            else:  # Speed_test's three calls, each its own launch: split, Discrete.sample, env.step
+                ks = split_keys(kbuf[k % 2].reshape(1, 2), key_n + 1)[0]
+                kbuf[(k + 1) % 2].copy_(ks[0])
+                sk = ks[1 + key_e0:1 + key_e0 + E].contiguous()
+                env.step(sk, state, env.sample_actions(sk), params)
+            nstep[0] = k + 1
+            n_steps -= n
 
-    run(args.warmup)
+    def restart():  # rollout(state0, master_key): back to the reset state and the master key
+        state.buf.copy_(state0)
+        kbuf[0].copy_(master0)
+        nstep[0] = 0
+
+    run(args.warmup)                          # Speed_test's compile run
+    restart()
     torch.cuda.synchronize()
-    G = (args.graph_steps if args.graph_steps > 0 and args.graph_steps % 2 == 0 and args.mode == "rollout"
-         and T == 1 else 0)
-    graph = None
-    if G:
-        # G consecutive launches in one HIP graph; G is even, so the key ping-pong buffers line up
-        # between replays (every launch's pointers are baked in at capture)
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            one_step()
-            one_step()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for _ in range(G):
-                one_step()
-        graph.replay()                        # one untimed replay (graph upload)
-        torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     D.barrier(R)
     torch.cuda.synchronize()
     D.barrier(R)
     t0 = time.perf_counter()
-    ev0.record()                              # on the launch stream (torch's current stream)
-    done = 0
-    if graph is not None:
-        for _ in range(args.steps // G):
-            graph.replay()
-        done = args.steps // G * G
-    run(args.steps - done)
-    ev1.record()
+    ev0.record(stream)                        # on the launch stream (slice 0 runs on it; the others join it)
+    run(args.steps)
+    ev1.record(stream)
     torch.cuda.synchronize()
     D.barrier(R)
     elapsed = time.perf_counter() - t0
-    # HIP events on the launch stream bracket the timed region.  Full-batch launches: the
-    # average k_env_step duration.  Sliced: per batched step (each k_env_step launch then
-    # covers one slice; rocprof's per-launch average is ~the slice's share of it).
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    # (step mode: the three launches of one step together; rocprof splits them)
-    elapsed = D.max_over_ranks(R, elapsed, device="cuda")
+    kern_ms = ev0.elapsed_time(ev1) / args.steps     # HIP-event time of the timed region per batched step
+    elapsed = D.max_over_ranks(R, elapsed, device=dev)
 
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        thr = args.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
+        cpu, cpu_state = cpu_baseline(env, day, state0, master0, thr)
+        restart()                             # the same rollout on the GPU, for the parity check
+        run(CPU_STEPS)
+        torch.cuda.synchronize()
+        cpu["parity"] = compare_states(env, cpu_state, state.buf.cpu().numpy())
     if rank != 0:
         D.finalize(R)
-        return
+        return 0
     value = world * E * args.steps / elapsed
     per_env = algorithmic_bytes_per_env_step(env)
     achieved = per_env * E / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            t = json.load(f)
-        if t.get("hbm_bytes_per_env_step") is not None:   # per batched env step, like `achieved`
-            traffic = round(t["hbm_bytes_per_env_step"] * E)
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        n_env_cpu, n_steps_cpu = 4096, 64       # one full episode (incl. auto-reset) of the metric workload
-        v, thr = cpu_baseline(env, day, n_env_cpu, n_steps_cpu, args.cpu_threads)
-        v1, _ = cpu_baseline(env, day, 512, 16, 1)
-        cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": thr, "kind": "port",
-               "sample": f"{n_env_cpu} envs x {n_steps_cpu} steps of the same config/day, C oracle (OpenMP)",
-               "single_core_value": round(v1, 1), "single_core_sample": "512 envs x 16 steps, 1 thread"}
+    metric_cfg = args.config == CONFIG and not args.agents and not args.n_data_msg
+    prof = _profile("r02_kernel_profile.json") if metric_cfg and args.mode == "rollout" else None
+    traffic = round(prof["hbm_bytes_per_env_step"] * E) if prof and prof.get("hbm_bytes_per_env_step") else None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
+                "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env,
+                "units_per_launch": E, "launches_per_step": args.slices if args.mode == "rollout" else 3}
+    issue = None
+    if prof:
+        roofline["rocprof"] = {k: prof[k] for k in ("kernel_avg_us", "launches", "envs_per_launch",
+                                                    "launches_in_flight", "source") if k in prof}
+        if prof.get("salu_per_env_step"):
+            # the CU's one scalar ALU, shared by its waves, is the scarcest pipe (DESIGN.md section 4)
+            a = prof["salu_per_env_step"] * world * E * args.steps / elapsed / N_CU / world
+            issue = {"bound": "salu_issue", "achieved": round(a / 1e9, 4), "peak": CLOCK_HZ / 1e9,
+                     "unit": "G SALU instr/s per CU", "frac": round(a / CLOCK_HZ, 4),
+                     "salu_per_env_step": prof["salu_per_env_step"], "source": prof.get("source")}
+    workload = (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, {env.num_msgs_per_step} msgs/step, "
+                "auto-reset, Speed_test semantics" if metric_cfg else
+                f"{args.config}.json agents {list(cfg.number_of_agents_per_type)}, {env.num_msgs_per_step} msgs/step, "
+                "auto-reset, Speed_test semantics")
     line = {
         "metric": "env steps/sec (whole node), 2-agent MARL, 10-level LOB, NUM_ENVS=4096",
         "value": round(value, 1),
@@ -236,23 +346,19 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": f"synthetic LOBSTER day ({args.n_msgs} msgs, PCG64 seed 20260403, mid {args.mid})",
-        "config": {"workload": (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, 112 msgs/step, "
-                                f"auto-reset, Speed_test semantics") if args.config == CONFIG else
-                               f"{args.config}.json, {env.num_msgs_per_step} msgs/step, auto-reset, Speed_test semantics",
-                   "num_envs_per_gpu": E, "num_envs_total": world * E, "parallelism": f"dp{world} (env shards)",
-                   "launch": (f"hipGraph of {G} steps" if G else
-                              (f"eager, {args.slices} env slices on their own streams (rollout_sampled, "
-                               f"{T} steps per call)" if sliced else "eager")),
-                   "mode": args.mode},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
-                     "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "slices": args.slices if sliced else 1,
-                     "bytes_per_env_step": per_env},
+        "config": {"workload": workload, "num_envs_per_gpu": E, "num_envs_total": world * E,
+                   "parallelism": f"dp{world} (env shards of one {world * E}-env Speed_test rollout)",
+                   "launch": (f"{args.slices} env slices on their own streams, {T} steps per rollout_sampled call"
+                              if args.mode == "rollout" else "split_keys + sample_actions + env.step per step"),
+                   "mode": args.mode, "seeds": "Speed_test: split(PRNGKey(0), NUM_ENVS + 1)"},
+        "roofline": roofline,
+        "issue_roofline": issue,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
     D.finalize(R)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

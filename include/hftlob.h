@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HFTLOB_ABI_VERSION 5
+#define HFTLOB_ABI_VERSION 6
 
 #define HFTLOB_OK            0
 #define HFTLOB_EINVAL      (-1)   /* bad config value / unsupported option */
@@ -270,23 +270,33 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, con
 /* n_steps consecutive Speed_test rollout steps — replaces the whole
  * jax.lax.scan of Speed_test.py:186-196 (`rollout`): the same results, bit for
  * bit, as n_steps hftlob_env_step_sampled calls with key_out fed back as
- * key_in.  The envs are cut into n_slices (1..4) contiguous slices: slice 0
- * is stepped on `stream`, the others on library-owned HIP streams forked from
- * / joined back to it with events (no host synchronisation), so one slice's
- * slowest envs overlap the other slices' next steps.  per_step != 0: out->{obs,rewards,done_all,
- * dones,info} and actions_out hold a leading [n_steps] dimension (step t at
- * offset t * their per-step size); per_step == 0: each step overwrites them
- * (the scan discards them).  key_out receives the master key after n_steps
- * splits.  The slice streams, events and key buffers are per device: calls
- * for one device must be issued from one host thread at a time and on one
- * caller stream (successive calls on that stream are ordered by the fork /
- * join events; calls overlapping on different caller streams would share the
- * slice key buffers). */
-int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, int n_steps,
-                               const uint32_t* key_in, uint32_t* key_out, int32_t* actions_out,
-                               const int32_t* msg_data, const int32_t* init_states, int32_t* state,
-                               const hftlob_step_out* out /*[host] struct*/, int per_step, int n_slices,
-                               void* stream);
+ * key_in.  Env e of this call takes the step key
+ * split(master, key_n + 1)[key_e0 + e + 1]: a call over the whole batch has
+ * key_e0 = 0, key_n = n_env; a rank that owns envs [key_e0, key_e0 + n_env)
+ * of a NUM_ENVS = key_n batch sharded over GPUs (ippo_rnn_JAXMARL_pmap.py:292-332)
+ * passes its offset, so N ranks together replay the single-device rollout.
+ * The envs are cut into n_slices (1..4) contiguous slices: slice 0 is stepped
+ * on `stream`, the others on library-owned HIP streams of the stream's device,
+ * forked from / joined back to it with events (no host synchronisation), so
+ * one slice's slowest envs overlap the other slices' next steps.
+ * key_scratch: uint32 [n_slices][2][2] device scratch owned by the caller (each
+ * slice's copy of the master-key chain); one buffer per concurrent caller stream.
+ * per_step != 0: out->{obs,rewards,done_all,dones,info} and actions_out hold a
+ * leading [n_steps] dimension (step t at offset t * their per-step size);
+ * per_step == 0: each step overwrites them (the scan discards them).  key_out
+ * receives the master key after n_steps splits.  The slice streams are created
+ * on first use; call hftlob_rollout_prepare before capturing a rollout in a
+ * hipGraph.  If a launch fails, the slices already enqueued are still joined
+ * back into `stream` before the error is returned. */
+int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, int key_e0, int key_n, int n_steps,
+                               const uint32_t* key_in, uint32_t* key_out, uint32_t* key_scratch,
+                               int32_t* actions_out, const int32_t* msg_data, const int32_t* init_states,
+                               int32_t* state, const hftlob_step_out* out /*[host] struct*/, int per_step,
+                               int n_slices, void* stream);
+
+/* Creates the library streams / events hftlob_env_rollout_sampled needs for n_slices
+ * slices on the device of `stream` (host-only; idempotent). */
+int hftlob_rollout_prepare(int n_slices, void* stream);
 
 /* Speed_test action sampling (Speed_test.py:166-177, gymnax Discrete.sample):
  * for env e with step key k_e,

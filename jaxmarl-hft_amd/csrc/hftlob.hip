@@ -2602,65 +2602,102 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg, int n_env, const uint32_t
 // events).  A step's launch waits only for the same slice's previous step, so
 // the slow envs at the end of one slice's step overlap the other slices' next
 // steps instead of idling the CUs at every step boundary.  Every slice carries
-// its own copy of the master key chain in a private ping-pong pair.
+// its own copy of the master key chain in a ping-pong pair of the CALLER's
+// key_scratch buffer (so rollouts on different caller streams never share
+// device scratch).  The library's slice streams are created per device, on
+// first use and only as many as the slices need (GPU_MAX_HW_QUEUES is 4).
 #define ROLLOUT_MAX_SLICES 4
 struct RolloutCtx {
-    bool ready = false;
+    int n_streams = 0;               // library streams created so far (slices 1..n_streams)
+    bool fork_ready = false;
     hipStream_t s[ROLLOUT_MAX_SLICES];
     hipEvent_t fork, join[ROLLOUT_MAX_SLICES];
-    uint32_t* keys = nullptr;  // [slice][2 ping-pong][2]
 };
 static RolloutCtx g_rollout[64];
-
 static std::mutex g_rollout_mu;
 
-static int rollout_ctx(RolloutCtx** out) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(HFTLOB_ELAUNCH, "hipGetDevice");
-    std::lock_guard<std::mutex> lock(g_rollout_mu);  // one-time creation of the device's streams / buffers
+// Device of the caller's stream (the null stream: the current device); the
+// calls below run with that device current and restore the caller's after.
+struct DeviceGuard {
+    int prev = -1, dev = 0;
+    int enter(hipStream_t st) {
+        if (hipGetDevice(&prev) != hipSuccess) return fail(HFTLOB_ELAUNCH, "hipGetDevice");
+        dev = prev;
+        if (st && hipStreamGetDevice(st, &dev) != hipSuccess) return fail(HFTLOB_ELAUNCH, "hipStreamGetDevice");
+        if (dev < 0 || dev >= 64) return fail(HFTLOB_ELAUNCH, "device index out of range");
+        if (dev != prev && hipSetDevice(dev) != hipSuccess) return fail(HFTLOB_ELAUNCH, "hipSetDevice");
+        return HFTLOB_OK;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// the device's slice streams 1..G-1 and events; created outside any stream capture
+// by hftlob_rollout_prepare (or lazily here).  A partial failure destroys what it made.
+static int rollout_ctx(int dev, int G, RolloutCtx** out) {
+    std::lock_guard<std::mutex> lock(g_rollout_mu);
     RolloutCtx& r = g_rollout[dev];
-    if (!r.ready) {
-        for (int g = 0; g < ROLLOUT_MAX_SLICES; ++g) {
-            if (hipStreamCreateWithFlags(&r.s[g], hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&r.join[g], hipEventDisableTiming) != hipSuccess)
-                return fail(HFTLOB_ELAUNCH, "rollout stream/event creation");
+    if (!r.fork_ready) {
+        if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess)
+            return fail(HFTLOB_ELAUNCH, "rollout fork event creation");
+        r.fork_ready = true;
+    }
+    while (r.n_streams < G - 1) {
+        const int g = r.n_streams + 1;
+        if (hipStreamCreateWithFlags(&r.s[g], hipStreamNonBlocking) != hipSuccess)
+            return fail(HFTLOB_ELAUNCH, "rollout stream creation");
+        if (hipEventCreateWithFlags(&r.join[g], hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(r.s[g]);
+            return fail(HFTLOB_ELAUNCH, "rollout join event creation");
         }
-        if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess ||
-            hipMalloc(&r.keys, sizeof(uint32_t) * 4 * ROLLOUT_MAX_SLICES) != hipSuccess)
-            return fail(HFTLOB_ELAUNCH, "rollout event / key buffer");
-        r.ready = true;
+        r.n_streams = g;
     }
     *out = &r;
     return HFTLOB_OK;
 }
 
-int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int n_steps, const uint32_t* key_in,
-                               uint32_t* key_out, int32_t* actions_out, const int32_t* msg_data,
-                               const int32_t* init_states, int32_t* state, const hftlob_step_out* out, int per_step,
-                               int n_slices, void* stream) {
+int hftlob_rollout_prepare(int n_slices, void* stream) {
+    if (n_slices < 1 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 1..4");
+    DeviceGuard dg;
+    int rc = dg.enter((hipStream_t)stream);
+    if (rc) return rc;
+    RolloutCtx* R = nullptr;
+    return rollout_ctx(dg.dev, n_slices, &R);
+}
+
+int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int key_e0, int key_n, int n_steps,
+                               const uint32_t* key_in, uint32_t* key_out, uint32_t* key_scratch,
+                               int32_t* actions_out, const int32_t* msg_data, const int32_t* init_states,
+                               int32_t* state, const hftlob_step_out* out, int per_step, int n_slices, void* stream) {
     int rc = check_env(cfg);
     if (rc) return rc;
     if (n_env < 0 || n_steps < 0) return fail(HFTLOB_ESHAPE, "negative n_env / n_steps");
+    if (key_e0 < 0 || key_n < key_e0 + n_env) return fail(HFTLOB_ESHAPE, "key_e0 / key_n: need 0 <= key_e0, key_e0 + n_env <= key_n");
     if (n_slices < 1 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 1..4");
     if (n_env == 0 || n_steps == 0) return HFTLOB_OK;
-    if (!key_in || !key_out || !msg_data || !init_states || !state || !out) return fail(HFTLOB_ENULL, "null array");
+    if (!key_in || !key_out || !key_scratch || !msg_data || !init_states || !state || !out)
+        return fail(HFTLOB_ENULL, "null array");
     if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
     if (key_in == key_out) return fail(HFTLOB_EINVAL, "key_in and key_out must be distinct buffers");
-    RolloutCtx* R = nullptr;
-    if ((rc = rollout_ctx(&R))) return rc;
     const int G = n_slices < n_env ? n_slices : n_env;
     hipStream_t caller = (hipStream_t)stream;
-    if (G > 1) {
-        if (hipEventRecord(R->fork, caller) != hipSuccess) return fail(HFTLOB_ELAUNCH, "fork event");
-    }
+    DeviceGuard dg;
+    if ((rc = dg.enter(caller))) return rc;
+    RolloutCtx* R = nullptr;
+    if ((rc = rollout_ctx(dg.dev, G, &R))) return rc;
+    if (G > 1 && hipEventRecord(R->fork, caller) != hipSuccess) return fail(HFTLOB_ELAUNCH, "fork event");
     const size_t na = (size_t)cfg->n_agents;
-    for (int g = 0; g < G; ++g) {
+    int forked = 1;  // slices whose stream waits on the fork (slice 0 runs on the caller's stream)
+    for (int g = 0; g < G && !rc; ++g) {
         const int e0 = (int)((long)n_env * g / G), e1 = (int)((long)n_env * (g + 1) / G), ne = e1 - e0;
-        // slice 0 runs on the caller's stream (one hardware queue fewer: GPU_MAX_HW_QUEUES is 4)
         hipStream_t st = g > 0 ? R->s[g] : caller;
-        if (g > 0 && hipStreamWaitEvent(st, R->fork, 0) != hipSuccess) return fail(HFTLOB_ELAUNCH, "fork wait");
-        uint32_t* kb = R->keys + 4 * g;  // this slice's ping-pong pair
-        for (int t = 0; t < n_steps; ++t) {
+        if (g > 0) {
+            if (hipStreamWaitEvent(st, R->fork, 0) != hipSuccess) { rc = fail(HFTLOB_ELAUNCH, "fork wait"); break; }
+            forked = g + 1;
+        }
+        uint32_t* kb = key_scratch + 4 * g;  // this slice's ping-pong pair
+        for (int t = 0; t < n_steps && !rc; ++t) {
             const size_t o = per_step ? (size_t)t * n_env + e0 : (size_t)e0;
             hftlob_step_out so;
             so.obs = out->obs + o * na * cfg->obs_stride;
@@ -2671,16 +2708,17 @@ int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int n_steps
             const uint32_t* kin = t == 0 ? key_in : kb + 2 * ((t - 1) & 1);
             uint32_t* kout = t == n_steps - 1 ? (g == 0 ? key_out : kb + 2 * (t & 1)) : kb + 2 * (t & 1);
             int32_t* acts = actions_out ? actions_out + o * cfg->action_words : nullptr;
-            rc = env_step_launch(cfg, ne, e0, n_env, nullptr, kin, kout, acts, msg_data, init_states,
+            rc = env_step_launch(cfg, ne, key_e0 + e0, key_n, nullptr, kin, kout, acts, msg_data, init_states,
                                  state + (size_t)e0 * cfg->rec_words, &so, st);
-            if (rc) return rc;
         }
     }
-    for (int g = 1; g < G; ++g) {  // join after every slice is enqueued (the caller's own slice 0 included)
+    // join every forked slice back into the caller's stream, also after a failed launch, so
+    // the caller stays ordered after the work already enqueued (and a capture stays joined)
+    for (int g = 1; g < forked; ++g) {
         if (hipEventRecord(R->join[g], R->s[g]) != hipSuccess || hipStreamWaitEvent(caller, R->join[g], 0) != hipSuccess)
-            return fail(HFTLOB_ELAUNCH, "join event");
+            if (!rc) rc = fail(HFTLOB_ELAUNCH, "join event");
     }
-    return HFTLOB_OK;
+    return rc;
 }
 
 int hftlob_sample_actions(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, int32_t* actions, void* stream) {

@@ -12,10 +12,10 @@ import os
 from .layout import EnvCfg, LobCfg, StepOut
 
 LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
-           "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_env_rollout_sampled", "hftlob_sample_actions",
-           "hftlob_split_keys")
+           "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_env_rollout_sampled", "hftlob_rollout_prepare",
+           "hftlob_sample_actions", "hftlob_split_keys")
 
 _lib = None
 
@@ -44,9 +44,11 @@ def lib() -> C.CDLL:
     L.hftlob_env_step.restype = i32
     L.hftlob_env_step_sampled.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp, vp, vp, vp, C.POINTER(StepOut), vp]
     L.hftlob_env_step_sampled.restype = i32
-    L.hftlob_env_rollout_sampled.argtypes = [C.POINTER(EnvCfg), i32, i32, vp, vp, vp, vp, vp, vp,
+    L.hftlob_env_rollout_sampled.argtypes = [C.POINTER(EnvCfg), i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp,
                                              C.POINTER(StepOut), i32, i32, vp]
     L.hftlob_env_rollout_sampled.restype = i32
+    L.hftlob_rollout_prepare.argtypes = [i32, vp]
+    L.hftlob_rollout_prepare.restype = i32
     L.hftlob_sample_actions.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp]
     L.hftlob_sample_actions.restype = i32
     L.hftlob_split_keys.argtypes = [i32, i32, i32, vp, vp, vp]
@@ -73,7 +75,9 @@ def ptr(t) -> int:
     return t.data_ptr()
 
 
-def stream_ptr(stream=None) -> int:
+def stream_ptr(stream=None, device=None) -> int:
+    """hipStream_t of `stream`, else of torch's current stream on `device` (default: the
+    current device)."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
     return s.cuda_stream

@@ -67,9 +67,10 @@ def book_process_(cfg: JAXLOB_Configuration, msgs: torch.Tensor, asks: torch.Ten
         raise ValueError("keys must be int32 [E, 2]")
     L = _lib.lib()
     c = _lob(cfg, prng_partitionable)
-    _lib.check(L.hftlob_book_process(C.byref(c), E, M, _lib.ptr(keys), _lib.ptr(msgs), _lib.ptr(asks), _lib.ptr(bids),
-                                     _lib.ptr(trades), _lib.ptr(best_asks), _lib.ptr(best_bids),
-                                     _lib.stream_ptr(stream)))
+    with torch.cuda.device(msgs.device):
+        _lib.check(L.hftlob_book_process(C.byref(c), E, M, _lib.ptr(keys), _lib.ptr(msgs), _lib.ptr(asks),
+                                         _lib.ptr(bids), _lib.ptr(trades), _lib.ptr(best_asks), _lib.ptr(best_bids),
+                                         _lib.stream_ptr(stream, device=msgs.device)))
 
 
 def scan_through_entire_array_save_bidask(cfg: JAXLOB_Configuration, key, msg_array: torch.Tensor,

@@ -321,6 +321,12 @@ class MARLEnv:
             a += n_t
         return {"world": world, "agents": agents}
 
+    def _abi(self, fn: str, *args):
+        """Call libhftlob `fn` with this env's device current and torch's current stream OF THAT
+        DEVICE appended (the kernels, and the rollout's slice streams, follow the stream)."""
+        with torch.cuda.device(self.device):
+            _lib.check(getattr(_lib.lib(), fn)(*args, _lib.stream_ptr(device=self.device)))
+
     # ------------------------------------------------------------------ API
     def reset(self, key: torch.Tensor, params: Optional[MultiAgentParams] = None):
         """MARLEnv.reset / reset_env (marl_env.py:129-207, 763-770) for E envs."""
@@ -330,10 +336,9 @@ class MARLEnv:
         E = keys.shape[0]
         buf = torch.empty((E, self.layout.rec_words), dtype=torch.int32, device=self.device)
         o = self._outputs(E)
-        _lib.check(_lib.lib().hftlob_env_reset(C.byref(self.cfg_c), E, _lib.ptr(keys),
-                                               _lib.ptr(params.loaded_params.message_data),
-                                               _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(buf),
-                                               C.byref(o["struct"]), _lib.stream_ptr()))
+        self._abi("hftlob_env_reset", C.byref(self.cfg_c), E, _lib.ptr(keys),
+                  _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
+                  _lib.ptr(buf), C.byref(o["struct"]))
         return self._split_types(o["obs"], True), self._wrap(buf)
 
     reset_env = reset
@@ -347,10 +352,9 @@ class MARLEnv:
         E = keys.shape[0]
         acts = self._actions(actions, E)
         o = self._outputs(E)
-        _lib.check(_lib.lib().hftlob_env_step(C.byref(self.cfg_c), E, _lib.ptr(keys), _lib.ptr(acts),
-                                              _lib.ptr(params.loaded_params.message_data),
-                                              _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf),
-                                              C.byref(o["struct"]), _lib.stream_ptr()))
+        self._abi("hftlob_env_step", C.byref(self.cfg_c), E, _lib.ptr(keys), _lib.ptr(acts),
+                  _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
+                  _lib.ptr(state.buf), C.byref(o["struct"]))
         return self._results(o, state, E)
 
     def step_sampled(self, key_in: torch.Tensor, key_out: torch.Tensor, state: MultiAgentState,
@@ -364,10 +368,9 @@ class MARLEnv:
         if actions_out is not None and (tuple(actions_out.shape) != (E, self.action_words)
                                         or actions_out.dtype != torch.int32):
             raise ValueError("actions_out must be int32 [E, action_words]")
-        _lib.check(_lib.lib().hftlob_env_step_sampled(
-            C.byref(self.cfg_c), E, _lib.ptr(key_in), _lib.ptr(key_out), _lib.ptr(actions_out),
-            _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
-            _lib.ptr(state.buf), C.byref(o["struct"]), _lib.stream_ptr()))
+        self._abi("hftlob_env_step_sampled", C.byref(self.cfg_c), E, _lib.ptr(key_in), _lib.ptr(key_out),
+                  _lib.ptr(actions_out), _lib.ptr(params.loaded_params.message_data),
+                  _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf), C.byref(o["struct"]))
         return self._results(o, state, E)
 
     @staticmethod
@@ -377,9 +380,23 @@ class MARLEnv:
         than the step tails they hide (512 envs: -6 %)."""
         return 2 if n_env >= 2048 else 1
 
+    def prepare_rollout(self, n_slices: int) -> None:
+        """Create the library's slice streams for `n_slices` on this env's device (host-only).
+        rollout_sampled does it on first use; call this before capturing a rollout in a HIP graph."""
+        self._abi("hftlob_rollout_prepare", int(n_slices))
+
+    def _key_scratch(self) -> torch.Tensor:
+        """Device scratch of the rollout's per-slice key chains, one per (env, caller stream)."""
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        cache = self.__dict__.setdefault("_kscr", {})
+        if s not in cache:
+            cache[s] = torch.zeros(16, dtype=torch.int32, device=self.device)
+        return cache[s]
+
     def rollout_sampled(self, key_in: torch.Tensor, key_out: torch.Tensor, state: MultiAgentState,
                         params: MultiAgentParams, n_steps: int, per_step: bool = False,
-                        actions_out: Optional[torch.Tensor] = None, n_slices: Optional[int] = None):
+                        actions_out: Optional[torch.Tensor] = None, n_slices: Optional[int] = None,
+                        key_e0: int = 0, key_n: Optional[int] = None):
         """Speed_test's whole ``rollout`` scan (Speed_test.py:186-196): bit for bit
         ``n_steps`` calls of :meth:`step_sampled` with ``key_out`` fed back as ``key_in``,
         enqueued on the current stream without host synchronisation.  The envs run as
@@ -410,10 +427,11 @@ class MARLEnv:
             shape = (E, self.action_words)
         if actions_out is not None and (tuple(actions_out.shape) != shape or actions_out.dtype != torch.int32):
             raise ValueError(f"actions_out must be int32 {list(shape)}")
-        _lib.check(_lib.lib().hftlob_env_rollout_sampled(
-            C.byref(self.cfg_c), E, n_steps, _lib.ptr(key_in), _lib.ptr(key_out), _lib.ptr(actions_out),
-            _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
-            _lib.ptr(state.buf), C.byref(o["struct"]), int(per_step), int(n_slices), _lib.stream_ptr()))
+        self._abi("hftlob_env_rollout_sampled", C.byref(self.cfg_c), E, int(key_e0),
+                  int(E if key_n is None else key_n), n_steps, _lib.ptr(key_in), _lib.ptr(key_out),
+                  _lib.ptr(self._key_scratch()), _lib.ptr(actions_out), _lib.ptr(params.loaded_params.message_data),
+                  _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf), C.byref(o["struct"]),
+                  int(per_step), int(n_slices))
         if not per_step:
             return self._results(o, state, E)
         T = n_steps
@@ -438,8 +456,7 @@ class MARLEnv:
         (== [E, num_agents] unless an agent type has a MultiDiscrete space)."""
         keys = self._keys(key)
         acts = torch.empty((keys.shape[0], self.action_words), dtype=torch.int32, device=self.device)
-        _lib.check(_lib.lib().hftlob_sample_actions(C.byref(self.cfg_c), keys.shape[0], _lib.ptr(keys),
-                                                    _lib.ptr(acts), _lib.stream_ptr()))
+        self._abi("hftlob_sample_actions", C.byref(self.cfg_c), keys.shape[0], _lib.ptr(keys), _lib.ptr(acts))
         return acts
 
 
@@ -447,6 +464,7 @@ def split_keys(keys: torch.Tensor, n: int, partitionable: bool = True) -> torch.
     """jax.random.split per row: uint32 [E, 2] -> [E, n, 2] (device)."""
     keys = keys.contiguous()
     out = torch.empty((keys.shape[0], n, 2), dtype=keys.dtype, device=keys.device)
-    _lib.check(_lib.lib().hftlob_split_keys(keys.shape[0], n, int(partitionable), _lib.ptr(keys), _lib.ptr(out),
-                                            _lib.stream_ptr()))
+    with torch.cuda.device(keys.device):
+        _lib.check(_lib.lib().hftlob_split_keys(keys.shape[0], n, int(partitionable), _lib.ptr(keys), _lib.ptr(out),
+                                                _lib.stream_ptr(device=keys.device)))
     return out

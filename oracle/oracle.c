@@ -1667,3 +1667,38 @@ int oracle_set_threads(int n) {
     return 1;
 #endif
 }
+
+/* Speed_test's rollout (Speed_test.py:186-196) on the CPU, the loop in C:
+ *   per step t: master, *step_keys = split(master, key_n + 1)
+ *               env e (global index key_e0 + e): actions = Discrete.sample per agent
+ *               (Speed_test.py:166-177), then MARLEnv.step with auto-reset.
+ * The master-key chain is derived first; then every env runs all n_steps on one
+ * thread (OpenMP over envs).  `master` [2] is advanced in place; `state` is
+ * [n_env][rec_words], updated in place.  The CPU baseline of bench.py and the
+ * metric-shape parity tests use it (test infrastructure, like the rest of this file). */
+int oracle_rollout_sampled(const hftlob_env_cfg* c, int n_env, int key_e0, int key_n, int n_steps, u32* master,
+                           const i32* msg_data, const i32* init_states, i32* state) {
+    if (!env_cfg_ok(c) || n_env < 0 || n_steps < 0 || key_e0 < 0 || key_n < key_e0 + n_env) return HFTLOB_EINVAL;
+    int part = c->prng_partitionable;
+    u32* chain = (u32*)malloc(sizeof(u32) * 2 * (size_t)(n_steps + 1));
+    if (!chain) return HFTLOB_EINVAL;
+    chain[0] = master[0];
+    chain[1] = master[1];
+    for (int t = 0; t < n_steps; ++t) oracle_split(chain + 2 * t, key_n + 1, 0, part, chain + 2 * (t + 1));
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int e = 0; e < n_env; ++e) {
+        float obs[HFTLOB_MAX_AGENTS * HFTLOB_MAX_OBS], rew[HFTLOB_MAX_AGENTS];
+        i32 dones[HFTLOB_MAX_AGENTS], acts[HFTLOB_MAX_AGENTS * 4], done_all;
+        i32* rec = state + (size_t)e * c->rec_words;
+        for (int t = 0; t < n_steps; ++t) {
+            u32 key[2];
+            oracle_split(chain + 2 * t, key_n + 1, key_e0 + e + 1, part, key);
+            oracle_sample_actions(c, 1, key, acts);
+            env_step_one(c, key, acts, msg_data, init_states, rec, obs, rew, &done_all, dones, NULL);
+        }
+    }
+    master[0] = chain[2 * n_steps];
+    master[1] = chain[2 * n_steps + 1];
+    free(chain);
+    return HFTLOB_OK;
+}

@@ -22,28 +22,40 @@ def build() -> str:
     return LIB
 
 
+def _bind(L):
+    vp = C.c_void_p
+    L.oracle_book_process.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp]
+    L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
+    L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
+    L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp]
+    L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
+    L.oracle_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)] * 2
+    L.oracle_randint.argtypes = [vp, C.c_int32, C.c_int32, C.c_int]
+    L.oracle_randint.restype = C.c_int32
+    L.oracle_permutation.argtypes = [vp, C.c_int, C.c_int, vp]
+    L.oracle_abi_layout.argtypes = [vp]
+    L.oracle_set_threads.argtypes = [C.c_int]
+    L.oracle_set_threads.restype = C.c_int
+    L.oracle_rollout_sampled.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB):
             build()
-        L = C.CDLL(LIB)
-        vp = C.c_void_p
-        L.oracle_book_process.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp]
-        L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
-        L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
-        L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
-        L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp]
-        L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
-        L.oracle_threefry2x32.argtypes = [C.c_uint32] * 4 + [C.POINTER(C.c_uint32)] * 2
-        L.oracle_randint.argtypes = [vp, C.c_int32, C.c_int32, C.c_int]
-        L.oracle_randint.restype = C.c_int32
-        L.oracle_permutation.argtypes = [vp, C.c_int, C.c_int, vp]
-        L.oracle_abi_layout.argtypes = [vp]
-        L.oracle_set_threads.argtypes = [C.c_int]
-        L.oracle_set_threads.restype = C.c_int
-        _lib = L
+        _lib = _bind(C.CDLL(LIB))
     return _lib
+
+
+def native_lib(path: str):
+    """The same restatement built -O3 -march=native for THIS host (`make native`), bench.py's
+    CPU baseline; compiled on first use into `path`."""
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", HERE, "-s", "native", f"NATIVE_OUT={path}"], check=True)
+    return _bind(C.CDLL(path))
 
 
 def _p(a):
@@ -164,3 +176,15 @@ def init_states(env_cfg_lob, windows, msgs, world_cfg, init_rec_words):
     t0 = np.full((W, world_cfg.nTrades, 8), -1, np.int32)
     a, b, t, _, _ = book_process(env_cfg_lob, im, a0, a0, t0, save_best=False)
     return loaded_rows(a, b, t, ft, windows, world_cfg.n_data_msg_per_step, init_rec_words, world_cfg)
+
+
+def rollout_sampled(env_cfg, master, msg_data, init_states, state, n_steps, key_e0=0, key_n=None, L=None):
+    """Speed_test's rollout on the CPU (oracle_rollout_sampled, the loop in C): returns
+    (state', master'); inputs are not modified.  L: a library handle (default: the checker)."""
+    st = np.array(state, dtype=np.int32, copy=True, order="C")
+    m = np.array(master, dtype=np.uint32, copy=True).reshape(2)
+    E = st.shape[0]
+    _chk((L or lib()).oracle_rollout_sampled(C.byref(env_cfg), E, int(key_e0), int(E if key_n is None else key_n),
+                                             int(n_steps), _p(m), _p(np.ascontiguousarray(msg_data, np.int32)),
+                                             _p(np.ascontiguousarray(init_states, np.int32)), _p(st)))
+    return st, m

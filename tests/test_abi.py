@@ -80,19 +80,26 @@ def test_error_null_and_shape(L):
     assert L.hftlob_env_step_sampled(C.byref(c), 4, k, None, None, k, k, k, C.byref(out), None) == -2
     assert L.hftlob_env_step_sampled(C.byref(c), 4, k, k, None, k, k, k, C.byref(out), None) == -1  # key_in == key_out
     assert L.hftlob_sample_actions(None, 4, None, None, None) == -2
-    # hftlob_env_rollout_sampled: argument checks run before any HIP call
+    # hftlob_env_rollout_sampled(cfg, n_env, key_e0, key_n, n_steps, key_in, key_out, key_scratch, actions,
+    #   msgs, init, state, out, per_step, n_slices, stream): argument checks run before any HIP call
     R = L.hftlob_env_rollout_sampled
-    assert R(None, 4, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -2            # null cfg
-    assert R(C.byref(c), -1, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3     # negative n_env
-    assert R(C.byref(c), 4, -1, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3     # negative n_steps
-    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(out), 0, 0, None) == -1      # n_slices 0
-    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(out), 0, 5, None) == -1      # n_slices > 4
-    assert R(C.byref(c), 0, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0       # empty batch
-    assert R(C.byref(c), 4, 0, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0       # no steps
-    assert R(C.byref(c), 4, 8, k, None, None, k, k, k, C.byref(out), 0, 2, None) == -2   # null key_out
-    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -2      # null outputs
+    assert R(None, 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -2           # null cfg
+    assert R(C.byref(c), -1, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3    # negative n_env
+    assert R(C.byref(c), 4, 0, 4, -1, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3    # negative n_steps
+    assert R(C.byref(c), 4, 2, 5, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3     # key_e0 + n_env > key_n
+    assert R(C.byref(c), 4, -1, 8, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3    # negative key_e0
+    assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 0, None) == -1     # n_slices 0
+    assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 5, None) == -1     # n_slices > 4
+    assert R(C.byref(c), 0, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0      # empty batch
+    assert R(C.byref(c), 4, 0, 4, 0, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0      # no steps
+    assert R(C.byref(c), 4, 0, 4, 8, k, None, k, None, k, k, k, C.byref(out), 0, 2, None) == -2  # null key_out
+    assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -2     # null outputs
     full = StepOut(k, k, k, k, None)
-    assert R(C.byref(c), 4, 8, k, k, None, k, k, k, C.byref(full), 0, 2, None) == -1     # key_in == key_out
+    k2 = C.c_void_p(128)
+    assert R(C.byref(c), 4, 0, 4, 8, k, k2, None, None, k, k, k, C.byref(full), 0, 2, None) == -2  # null scratch
+    assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(full), 0, 2, None) == -1    # key_in == key_out
+    assert L.hftlob_rollout_prepare(0, None) == -1
+    assert L.hftlob_rollout_prepare(5, None) == -1
 
 
 @pytest.mark.parametrize("field,value,code", [("cancel_mode", 4, -1), ("type_4_interpretation", 3, -1),

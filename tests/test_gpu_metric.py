@@ -1,0 +1,72 @@
+"""Parity at the metric's exact shape and launch path (bench.py):
+2_player_fq_fqc.json, NUM_ENVS = 4096, the 400k-message synthetic day (mid 2 M and 28 M: the
+GOOG-like regime rounds prices above 2^24 in float32), Speed_test's seeds
+(master_key, *reset_keys = split(PRNGKey(0), NUM_ENVS + 1), Speed_test.py:147) and its rollout
+(Speed_test.py:186-196) as the bench runs it: MARLEnv.rollout_sampled over 2 env slices on their
+own streams, 66 steps (the 64-step episode's auto-reset included).  The end state (every integer
+word bit-exact, float words within 1e-5) and the carried master key must equal the CPU oracle's
+rollout of the same workload.  Also: a rank's shard of a rollout (key_e0 / key_n, bench.py
+--gpus N) equals its rows of the whole-batch rollout."""
+import numpy as np
+import pytest
+import torch
+
+from hftlob.config_io import builtin_config
+from hftlob.data.synthetic import generate_day
+from hftlob.env import MARLEnv, split_keys
+from oracle import pyoracle as O
+from test_gpu_env import _compare_state, _day
+
+pytestmark = pytest.mark.gpu
+
+_METRIC_DAYS = {}
+
+
+def _metric_day(mid):
+    if mid not in _METRIC_DAYS:
+        _METRIC_DAYS[mid] = generate_day(n_msgs=400_000, mid=mid, snap_every=6400)
+    return _METRIC_DAYS[mid]
+
+
+@pytest.mark.parametrize("mid", [2_000_000, 28_000_000])
+def test_metric_shape_rollout_parity(mid):
+    cfg = builtin_config("2_player_fq_fqc")
+    day = _metric_day(mid)
+    env = MARLEnv(None, cfg, data=day, return_info=False, persistent_outputs=True)
+    params = env.default_params
+    init = O.init_states(env.cfg_c.lob, env.windows, day.msgs, cfg.world_config, env.layout.init_rec_words)
+    assert (init == env._init_states.cpu().numpy()).all()
+    E, T = 4096, 66
+    all_keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device="cuda"), E + 1)[0]
+    o_keys = O.split_keys(np.zeros((1, 2), np.uint32), E + 1)[0]
+    assert (all_keys.cpu().numpy().view(np.uint32) == o_keys).all(), "Speed_test key split"
+    _, state = env.reset(all_keys[1:].contiguous(), params)
+    o_state, _ = O.env_reset(env.cfg_c, o_keys[1:], init)
+    _compare_state(env, o_state, state.buf.cpu().numpy(), "reset")
+    kin, kout = all_keys[0].clone(), torch.empty(2, dtype=torch.int32, device="cuda")
+    env.rollout_sampled(kin, kout, state, params, T, n_slices=2)       # the bench's launch path
+    torch.cuda.synchronize()
+    o_end, o_master = O.rollout_sampled(env.cfg_c, o_keys[0], day.msgs, init, o_state, T)
+    _compare_state(env, o_end, state.buf.cpu().numpy(), f"after {T} steps")
+    assert (kout.cpu().numpy().view(np.uint32) == o_master).all(), "carried master key"
+    # the rollout crossed every env's episode end: each record restarted (step counter < T)
+    assert (state.world_state.step_counter.cpu().numpy() < T).all()
+
+
+def test_rollout_shards_equal_whole_batch():
+    """bench.py --gpus N: rank r steps envs [r*E, (r+1)*E) with key_e0 = r*E, key_n = N*E; the
+    shards together are the whole-batch rollout, bit for bit (state and carried key)."""
+    cfg = builtin_config("2_player_fq_fqc")
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000), persistent_outputs=True)
+    params = env.default_params
+    E, N, T = 48, 3, 12
+    keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device="cuda"), N * E + 1)[0]
+    _, whole = env.reset(keys[1:].contiguous(), params)
+    shards = [env._wrap(whole.buf[r * E:(r + 1) * E].clone()) for r in range(N)]
+    kout = torch.empty(2, dtype=torch.int32, device="cuda")
+    env.rollout_sampled(keys[0].clone(), kout, whole, params, T, n_slices=2)
+    for r, s in enumerate(shards):
+        ko = torch.empty(2, dtype=torch.int32, device="cuda")
+        env.rollout_sampled(keys[0].clone(), ko, s, params, T, n_slices=1 + r % 2, key_e0=r * E, key_n=N * E)
+        assert (ko == kout).all(), f"rank {r}: carried key"
+        assert (s.buf == whole.buf[r * E:(r + 1) * E]).all(), f"rank {r}: state"
