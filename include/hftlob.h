@@ -275,12 +275,17 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, con
  * key_e0 = 0, key_n = n_env; a rank that owns envs [key_e0, key_e0 + n_env)
  * of a NUM_ENVS = key_n batch sharded over GPUs (ippo_rnn_JAXMARL_pmap.py:292-332)
  * passes its offset, so N ranks together replay the single-device rollout.
- * The envs are cut into n_slices (1..4) contiguous slices: slice 0 is stepped
- * on `stream`, the others on library-owned HIP streams of the stream's device,
- * forked from / joined back to it with events (no host synchronisation), so
- * one slice's slowest envs overlap the other slices' next steps.
+ * n_slices = 0: ONE kernel launch for all n_steps; every env (one wavefront)
+ * runs its steps back to back with its own copy of the master-key chain, so no
+ * step boundary waits for the batch's slowest env.
+ * n_slices = 1..4: the envs are cut into n_slices contiguous slices, each stepped
+ * by one launch per step: slice 0 on `stream`, the others on library-owned HIP
+ * streams of the stream's device, forked from / joined back to it with events
+ * (no host synchronisation), so one slice's slowest envs overlap the other
+ * slices' next steps.
  * key_scratch: uint32 [n_slices][2][2] device scratch owned by the caller (each
- * slice's copy of the master-key chain); one buffer per concurrent caller stream.
+ * slice's copy of the master-key chain; may be NULL for n_slices = 0); one buffer
+ * per concurrent caller stream.
  * per_step != 0: out->{obs,rewards,done_all,dones,info} and actions_out hold a
  * leading [n_steps] dimension (step t at offset t * their per-step size);
  * per_step == 0: each step overwrites them (the scan discards them).  key_out

@@ -2389,6 +2389,50 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
     if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
 
+// Speed_test's whole rollout scan in ONE launch (Speed_test.py:186-196): every env
+// (one wave) runs its n_steps steps back to back, so no step boundary waits for the
+// batch's slowest env (a wave that finishes a step starts its next one at once).
+// Each wave carries its own copy of the master-key chain.  The step body is the
+// same env_step_dev as k_env_step; per-iteration opaque copies of the config and
+// base pointers keep LICM from hoisting the body's invariant loads and addresses
+// out of the step loop (they would stay live across it and double the registers):
+// the config pointer stays in the constant address space, so its fields are
+// still scalar loads, re-issued once per step.  (Never take &c: that copies the
+// struct to scratch.)
+typedef const __attribute__((address_space(4))) hftlob_env_cfg kcfg_t;
+template <int S, int NFIX, bool RC>
+__global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_env, int key_e0, int key_n, int n_steps,
+                                                    int per_step, const u32* __restrict__ master,
+                                                    u32* __restrict__ master_out, i32* __restrict__ actions_io,
+                                                    const i32* __restrict__ msg_data,
+                                                    const i32* __restrict__ init_states, i32* __restrict__ state,
+                                                    float* __restrict__ obs_out, float* __restrict__ rew_out,
+                                                    u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
+                                                    i32* __restrict__ info_out) {
+    extern __shared__ __attribute__((aligned(16))) i32 lds[];
+    const int e = blockIdx.x;
+    if (e >= n_env) return;
+    Key mk{master[0], master[1]};
+    // `c` is the first kernel argument: offset 0 of the kernarg segment (constant address space)
+    kcfg_t* kp = (kcfg_t*)__builtin_amdgcn_kernarg_segment_ptr();
+#pragma unroll 1
+    for (int t = 0; t < n_steps; ++t) {
+        const size_t o = per_step ? (size_t)t * n_env : 0;
+        kcfg_t* cp = kp;
+        i32* st = state;
+        const i32* md = msg_data;
+        const i32* is = init_states;
+        asm volatile("" : "+s"(cp), "+s"(st), "+s"(md), "+s"(is));
+        const hftlob_env_cfg& cc = *(const hftlob_env_cfg*)cp;
+        env_step_dev<S, NFIX, RC>(cc, key_n, key_e0 + e, e, nullptr, &mk,
+                                  actions_io ? actions_io + o * cc.action_words : nullptr, md, is, st,
+                                  obs_out + o * cc.n_agents * cc.obs_stride, rew_out + o * cc.n_agents,
+                                  done_all_out + o, dones_out + o * cc.n_agents,
+                                  info_out ? info_out + o * cc.info_words : nullptr, lds);
+    }
+    if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
+}
+
 // ==================================================== K3/K4: PRNG kernels
 __global__ void k_sample_actions(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys, i32* __restrict__ actions) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2572,6 +2616,31 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int
     return launch_status();
 }
 
+// all n_steps of a rollout in one k_env_rollout launch (see there)
+static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int key_n, int n_steps, int per_step,
+                              const uint32_t* key_in, uint32_t* key_out, int32_t* actions, const int32_t* msg_data,
+                              const int32_t* init_states, int32_t* state, const hftlob_step_out* out, void* stream) {
+    const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
+    hipStream_t st = (hipStream_t)stream;
+    dim3 g(n_env), b(64);
+    const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
+                            12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+#define LAUNCH_ROLL(SS, NF, RC) hipLaunchKernelGGL((k_env_rollout<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, \
+                                               n_steps, per_step, key_in, key_out, actions, msg_data, init_states, \
+                                               state, out->obs, out->rewards, out->done_all, out->dones, out->info)
+    if (cfg->lob.cancel_mode >= 2) {
+        if (S == 1) LAUNCH_ROLL(1, 0, true);
+        else if (S == 2) LAUNCH_ROLL(2, 0, true);
+        else LAUNCH_ROLL(4, 0, true);
+    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0 && !has_fixed_prices(cfg))
+        LAUNCH_ROLL(2, 100, false);
+    else if (S == 1) LAUNCH_ROLL(1, 0, false);
+    else if (S == 2) LAUNCH_ROLL(2, 0, false);
+    else LAUNCH_ROLL(4, 0, false);
+#undef LAUNCH_ROLL
+    return launch_status();
+}
+
 int hftlob_env_step(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const int32_t* actions,
                     const int32_t* msg_data, const int32_t* init_states, int32_t* state, const hftlob_step_out* out,
                     void* stream) {
@@ -2658,7 +2727,8 @@ static int rollout_ctx(int dev, int G, RolloutCtx** out) {
 }
 
 int hftlob_rollout_prepare(int n_slices, void* stream) {
-    if (n_slices < 1 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 1..4");
+    if (n_slices < 0 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 0..4");
+    if (n_slices <= 1) return HFTLOB_OK;  // no library stream needed
     DeviceGuard dg;
     int rc = dg.enter((hipStream_t)stream);
     if (rc) return rc;
@@ -2674,16 +2744,19 @@ int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int key_e0,
     if (rc) return rc;
     if (n_env < 0 || n_steps < 0) return fail(HFTLOB_ESHAPE, "negative n_env / n_steps");
     if (key_e0 < 0 || key_n < key_e0 + n_env) return fail(HFTLOB_ESHAPE, "key_e0 / key_n: need 0 <= key_e0, key_e0 + n_env <= key_n");
-    if (n_slices < 1 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 1..4");
+    if (n_slices < 0 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 0..4");
     if (n_env == 0 || n_steps == 0) return HFTLOB_OK;
-    if (!key_in || !key_out || !key_scratch || !msg_data || !init_states || !state || !out)
+    if (!key_in || !key_out || (n_slices > 0 && !key_scratch) || !msg_data || !init_states || !state || !out)
         return fail(HFTLOB_ENULL, "null array");
     if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
     if (key_in == key_out) return fail(HFTLOB_EINVAL, "key_in and key_out must be distinct buffers");
-    const int G = n_slices < n_env ? n_slices : n_env;
     hipStream_t caller = (hipStream_t)stream;
     DeviceGuard dg;
     if ((rc = dg.enter(caller))) return rc;
+    if (n_slices == 0)  // one launch: every env runs its n_steps back to back
+        return env_rollout_launch(cfg, n_env, key_e0, key_n, n_steps, per_step, key_in, key_out, actions_out,
+                                  msg_data, init_states, state, out, caller);
+    const int G = n_slices < n_env ? n_slices : n_env;
     RolloutCtx* R = nullptr;
     if ((rc = rollout_ctx(dg.dev, G, &R))) return rc;
     if (G > 1 && hipEventRecord(R->fork, caller) != hipSuccess) return fail(HFTLOB_ELAUNCH, "fork event");

@@ -196,6 +196,12 @@ void oracle_permutation(const u32* key, int n, int part, int* perm) {
 }
 
 /* ========================================================= order book (L1) */
+#ifdef ORACLE_STATS /* message-mix statistics (tools/msg_mix.py; single-threaded builds only) */
+long long oracle_stats[32];
+#define STAT(i) (oracle_stats[i]++)
+#else
+#define STAT(i) ((void)0)
+#endif
 typedef struct {
     i32 side, type, price, qty, oid, tid, t, tns;
 } Msg;
@@ -262,6 +268,11 @@ static void cancel_order(const hftlob_lob_cfg* c, i32* s, const Msg* m, const u3
     int nO = c->n_orders, idx = -1;
     for (int i = 0; i < nO; ++i)
         if (s[i * 6 + 2] == m->oid) { idx = i; break; }
+#ifdef ORACLE_STATS
+    STAT(10);
+    if (m->qty == 0) STAT(11);
+    else if (idx >= 0) STAT(12);
+#endif
     if (idx == -1) { /* get_init_id_match (called for every cancel mode) */
         i32 lo = wsub(c->init_id, wmul(c->book_depth, 2));
         for (int i = 0; i < nO; ++i) {
@@ -275,6 +286,18 @@ static void cancel_order(const hftlob_lob_cfg* c, i32* s, const Msg* m, const u3
         }
     }
     if (idx == -1) idx = nO - 1; /* negative index wraps to the last slot */
+#ifdef ORACLE_STATS
+    if (m->qty != 0) {
+        if (s[idx * 6 + 1] - m->qty <= 0) STAT(13);          /* row removed */
+        int bid = m->side == 1;
+        i32 best = bid ? -1 : c->maxint;
+        for (int i = 0; i < nO; ++i) {
+            i32 p = s[i * 6];
+            if (bid) best = imax(best, p); else if (p != -1) best = imin(best, p);
+        }
+        if (s[idx * 6] == best) STAT(14);                      /* at the best price */
+    }
+#endif
     s[idx * 6 + 1] = wsub(s[idx * 6 + 1], m->qty);
     remove_zero_neg(s, nO);
 }
@@ -340,6 +363,7 @@ static i32 match_against(const hftlob_lob_cfg* c, i32* s, int bid_side, i32 qtm,
         i32 tp = s[top * 6];
         int go = bid_side ? (tp >= price) : (tp <= price);
         if (!(go && qtm > 0 && tp != -1)) return qtm;
+        STAT(20);
         qtm = match_order(s, nO, top, qtm, m, trades, c->n_trades);
     }
 }
@@ -410,6 +434,14 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
     i32 s = m.side, t = m.type;
     int lim = (t == 1) || (t == 4), cnl = (t == 2) || (t == 3);
     int index = (s == 1 && lim) * 1 + (s == -1 && cnl) * 2 + (s == 1 && cnl) * 3 + (s == 0 && t == 0) * 4;
+#ifdef ORACLE_STATS
+    STAT(index);
+    if (t == 4) STAT(5);
+    if ((index == 0 || index == 1) && m.qty <= 0) STAT(6);
+    long long before = oracle_stats[20];
+    i32 ba0[2], bb0[2], ba1[2], bb1[2];
+    best_quotes(c, asks, bids, ba0, bb0);
+#endif
     switch (index) {
         case 0: ask_lim(c, m, asks, bids, trades); break;
         case 1: bid_lim(c, m, asks, bids, trades); break;
@@ -417,6 +449,14 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
         case 3: cancel_order(c, bids, &m, mk); break;
         default: break; /* doNothing */
     }
+#ifdef ORACLE_STATS
+    if ((index == 0 || index == 1) && oracle_stats[20] > before) STAT(7);   /* crossing */
+    best_quotes(c, asks, bids, ba1, bb1);
+    if (ba1[0] != ba0[0]) STAT(15);
+    if (bb1[0] != bb0[0]) STAT(16);
+    if (ba1[0] != ba0[0] || ba1[1] != ba0[1]) STAT(17);
+    if (bb1[0] != bb0[0] || bb1[1] != bb0[1]) STAT(18);
+#endif
 }
 
 static int lob_cfg_ok(const hftlob_lob_cfg* c) {

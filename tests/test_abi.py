@@ -88,7 +88,7 @@ def test_error_null_and_shape(L):
     assert R(C.byref(c), 4, 0, 4, -1, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3    # negative n_steps
     assert R(C.byref(c), 4, 2, 5, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3     # key_e0 + n_env > key_n
     assert R(C.byref(c), 4, -1, 8, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == -3    # negative key_e0
-    assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 0, None) == -1     # n_slices 0
+    assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, -1, None) == -1    # n_slices < 0
     assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 5, None) == -1     # n_slices > 4
     assert R(C.byref(c), 0, 0, 4, 8, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0      # empty batch
     assert R(C.byref(c), 4, 0, 4, 0, k, k, k, None, k, k, k, C.byref(out), 0, 2, None) == 0      # no steps
@@ -98,7 +98,7 @@ def test_error_null_and_shape(L):
     k2 = C.c_void_p(128)
     assert R(C.byref(c), 4, 0, 4, 8, k, k2, None, None, k, k, k, C.byref(full), 0, 2, None) == -2  # null scratch
     assert R(C.byref(c), 4, 0, 4, 8, k, k, k, None, k, k, k, C.byref(full), 0, 2, None) == -1    # key_in == key_out
-    assert L.hftlob_rollout_prepare(0, None) == -1
+    assert L.hftlob_rollout_prepare(-1, None) == -1
     assert L.hftlob_rollout_prepare(5, None) == -1
 
 

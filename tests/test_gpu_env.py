@@ -286,13 +286,18 @@ def test_step_sampled_equals_split_sample_step(name, part, exe):
         assert (da1 == d2["__all__"]).all()
 
 
-@pytest.mark.parametrize("name,part,exe,T,per_step,G", [("2_player_fq_fqc", True, None, 70, False, 4),
+@pytest.mark.parametrize("name,part,exe,T,per_step,G", [("2_player_fq_fqc", True, None, 70, False, 0),
+                                                          ("2_player_fq_fqc", True, None, 7, True, 0),
+                                                          ("3_player_fq_fqc_dir", False, None, 13, True, 0),
+                                                          ("exec_debug_fixed_quants_complex", False, 2, 9, True, 0),
+                                                          ("2_player_fq_fqc", True, None, 70, False, 4),
                                                           ("2_player_fq_fqc", True, None, 7, True, 3),
                                                           ("2_player_fq_fqc", True, None, 5, True, 1),
                                                           ("3_player_fq_fqc_dir", False, None, 13, True, 2),
                                                           ("exec_debug_fixed_quants_complex", False, 2, 9, True, 4)])
 def test_rollout_sampled_equals_step_sampled(name, part, exe, T, per_step, G):
-    """hftlob_env_rollout_sampled (T steps over G env slices on their own streams) == T
+    """hftlob_env_rollout_sampled (T steps over G env slices on their own streams; G = 0: one
+    k_env_rollout launch, every env's T steps back to back) == T
     hftlob_env_step_sampled launches: state, carried key, and (per_step) every step's
     actions / obs / rewards / dones, bit for bit; the rollout crosses an auto-reset."""
     cfg = builtin_config(name)

@@ -89,6 +89,18 @@ def report(d):
     names = sorted({k for v in disp.values() for k in v} - {"SQ_WAVES"})
     short = [n.replace("SQ_", "").replace("INSTS_", "I_").replace("ACTIVE_INST_", "A_").replace("ICACHE_", "IC_")
              for n in names]
+    # wall time per message of each dispatch (kernel trace of the same runs), 4096 envs in flight
+    dur = collections.defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)):
+        rows = [r for r in csv.DictReader(open(f))
+                if "k_book_process" in r["Kernel_Name"] and int(r.get("Grid_Size_X") or r.get("Grid_Size")) == E * 64]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        for kind, r in zip(KINDS, rows[-len(KINDS):]):
+            dur[kind].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / N)
+    if dur:
+        print("ns per message (whole batch of 4096 envs, min over passes):")
+        for kind in KINDS:
+            print(f"  {kind:18s} {min(dur[kind]):8.1f}")
     print("per message per wave (cycle counters in quad-cycles; SQC_* per message per CU-pair estimate):")
     print(f"{'':18s}" + "".join(f"{s:>10s}" for s in short))
     for kind in KINDS:
