@@ -112,6 +112,13 @@ DEV float wave_fsum(float v) {
     return __int_as_float(rdl(__float_as_int(v), 63));
 }
 DEV unsigned long long ballot(bool p) { return __ballot(p); }
+// A fresh copy of a uniform value: a comparison of it is then local to its one branch or
+// select (s_cmp + s_cbranch_scc / s_cselect) instead of a comparison shared by several uses,
+// which the compiler keeps as a 64-bit lane mask and tests with s_and_b64 exec at each use.
+DEV i32 fresh(i32 v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
 
 // Diagnostic build only (-DHFTLOB_STAMPS): per-phase shader-clock stamps of
 // k_env_step, written to the info buffer in place of the info fields.
@@ -234,7 +241,9 @@ struct Valid {  // slot (or trade row) r*64+lane exists
         const int l = lane_id();
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            v[r] = r * 64 + l < n;
+            // (the compiler does not know lane_id() < 64: state full register sets explicitly, so a
+            // compile-time n folds them away)
+            v[r] = (r + 1) * 64 <= n ? true : r * 64 + l < n;
             const int k = n - r * 64;
             m[r] = k >= 64 ? ~0ull : (k <= 0 ? 0ull : ((1ull << k) - 1ull));
         }
@@ -302,7 +311,17 @@ struct Side {
     i32* t;              // LDS table [6][R]
     i32* scr;            // LDS scratch row (64 words)
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid under F_OK
+    i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
+                         // every handler reads prices, only adds and row clears write them
 };
+
+// slot e of a lane-strided register column <- v (lane e & 63 of register e >> 6): one
+// compare and one select per register set, no scalar work
+template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int r = 0; r < S; ++r) c[r] = (l + 64 * r == e) ? v : c[r];
+}
 
 // Wave-uniform book flags, one SGPR bitfield (bools would each be a 64-bit
 // lane mask the compiler copies at every merge):
@@ -311,15 +330,23 @@ struct Side {
 //          ever has to look at the row just written
 //   NEG1   some row with p != -1 holds a -1 in another field (then "first row
 //          holding ANY -1" needs the full test, else p == -1 suffices)
-//   FAST   both sides CLEAN and neither NEG1 (the handlers' common variant)
-enum : u32 { F_OK_A = 1, F_OK_B = 2, F_CLEAN_A = 4, F_CLEAN_B = 8, F_NEG1_A = 16, F_NEG1_B = 32, F_FAST = 64 };
+//   PM1    some row with p == -1 holds a field != -1 (an order priced -1)
+//   FAST   both sides CLEAN, neither NEG1 nor PM1 (the handlers' common variant): then a
+//          row holds a -1 <=> its price is -1 <=> it is all -1, so the free slots are the
+//          p == -1 slots of the register price column
+// (bit 0 is left unused: a branch on a bit-0 test compiles to s_bitcmp1 + a 64-bit lane mask
+// + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc)
+enum : u32 { F_OK_A = 2, F_OK_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64, F_FAST = 128,
+             F_PM1_A = 256, F_PM1_B = 512 };
 template <bool ASKS> struct SideBits {
     static constexpr u32 OK = ASKS ? F_OK_A : F_OK_B;
     static constexpr u32 CLEAN = ASKS ? F_CLEAN_A : F_CLEAN_B;
     static constexpr u32 NEG1 = ASKS ? F_NEG1_A : F_NEG1_B;
+    static constexpr u32 PM1 = ASKS ? F_PM1_A : F_PM1_B;
 };
 DEV u32 fast_bit(u32 fl) {
-    return (fl & (F_CLEAN_A | F_CLEAN_B | F_NEG1_A | F_NEG1_B)) == (F_CLEAN_A | F_CLEAN_B) ? F_FAST : 0u;
+    return (fl & (F_CLEAN_A | F_CLEAN_B | F_NEG1_A | F_NEG1_B | F_PM1_A | F_PM1_B)) == (F_CLEAN_A | F_CLEAN_B)
+               ? F_FAST : 0u;
 }
 
 // A side's rows in registers between the global load and the LDS commit, so
@@ -344,7 +371,7 @@ template <int S> DEV void fetch_side(SideRows<S>& f, const i32* g, const Valid<S
 // max of the complemented fields (VALU), not as chains of lane-mask logic.
 template <bool ASKS, int S> DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) {
     const int l = lane_id();
-    lmask bad = 0, n1 = 0;
+    lmask bad = 0, n1 = 0, pm1 = 0;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         const int sl = r * 64 + l;
@@ -353,14 +380,17 @@ template <bool ASKS, int S> DEV u32 commit_side(Side<S>& s, const SideRows<S>& f
             i32* t = s.t + sl;
             t[FP * R] = p; t[FQ * R] = q; t[FOID * R] = oid; t[FTID * R] = tid; t[FTS * R] = ts; t[FTNS * R] = tns;
         }
+        s.pc[r] = V.v[r] ? p : -1;
         const u32 np = ~(u32)p, nq = ~(u32)q, no = ~(u32)oid, nt = ~(u32)tid, ns = ~(u32)ts, nn = ~(u32)tns;
         const u32 any0 = min(min(min(np, nq), min(no, nt)), min(ns, nn));  // 0 <=> some field == -1
         const u32 all0 = max(max(max(np, nq), max(no, nt)), max(ns, nn));  // 0 <=> every field == -1
         bad |= V.m[r] & bal((q <= 0) & (all0 != 0u));
         n1 |= V.m[r] & bal((p != -1) & (any0 == 0u));
+        pm1 |= V.m[r] & bal((p == -1) & (all0 != 0u));
     }
     lds_order();
-    return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u);
+    return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u) |
+           (pm1 != 0ull ? SideBits<ASKS>::PM1 : 0u);
 }
 template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
     SideRows<S> f;
@@ -381,14 +411,16 @@ template <int S> DEV void store_side(const Side<S>& s, i32* g, int R, const Vali
         }
     }
 }
-// clear every valid slot whose field-f value is selected by lane mask m
-template <int S> DEV void clear_masked(i32* t, int R, const lmask (&m)[S]) {
+// clear every valid slot selected by lane mask m (the LDS rows and the register price column)
+template <int S> DEV void clear_masked(Side<S>& s, int R, const lmask (&m)[S]) {
     const int l = lane_id();
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        if ((m[r] >> l) & 1ull) {
+        const bool hit = (m[r] >> l) & 1ull;
+        s.pc[r] = hit ? -1 : s.pc[r];
+        if (hit) {
 #pragma unroll
-            for (int f = 0; f < 6; ++f) t[f * R + r * 64 + l] = -1;
+            for (int f = 0; f < 6; ++f) s.t[f * R + r * 64 + l] = -1;
         }
     }
     lds_order();
@@ -403,7 +435,7 @@ template <bool ASKS, int S> DEV void rzn(Side<S>& s, u32& fl, int R, const Valid
     lmask m[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
-    clear_masked(s.t, R, m);
+    clear_masked(s, R, m);
     fl = (fl | SideBits<ASKS>::CLEAN) & ~SideBits<ASKS>::OK;
     fl = (fl & ~F_FAST) | fast_bit(fl);
 }
@@ -436,11 +468,10 @@ DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i3
 }
 // recompute a side's cached best quote (sets its OK bit)
 template <bool ASKS, int S> DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint) {
-    i32 p[S], q[S];
-    ldcol(s.t, R, FP, p);
+    i32 q[S];
     ldcol(s.t, R, FQ, q);
-    if (ASKS) best_ask_pq(p, q, V, maxint, s.best_p, s.best_q);
-    else best_bid_pq(p, q, V, s.best_p, s.best_q);
+    if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q);
+    else best_bid_pq(s.pc, q, V, s.best_p, s.best_q);
     fl |= SideBits<ASKS>::OK;
 }
 
@@ -542,7 +573,8 @@ struct Book {
 };
 
 // message handler codes (the reference's dispatch index) and flags, see decode_msgs
-enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8, H_NEG1 = 16 };
+enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8, H_NEG1 = 16,
+       H_PM1 = 32 };
 struct Msg {
     i32 h, side, price, qty, oid, tid, t, tns;  // h: handler code and H_* flags (decode_msgs)
 };
@@ -551,19 +583,33 @@ struct Msg {
 // side: it changes (best_p, best_q) only where get_best_* / get_volume_at_price
 // would, and falls back to a full recompute (ok = false) where it cannot tell.
 template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq, i32 maxint) {
-    // an all -1 row now holds (np, nq > 0)
+    // an all -1 row now holds (np, nq > 0).  Branches ordered for the common case, an order
+    // behind the best (one compare each); per side the cases are those of get_best_* with -1
+    // (and, for asks, maxint) standing for "no price".
     constexpr u32 OK = SideBits<!BID>::OK;
-    if (fl & OK) {
-        if (BID) {
-            if (s.best_p == -1) {
-                if (np > -1) { s.best_p = np; s.best_q = nq; } else fl &= ~OK;
-            } else if (np > s.best_p) { s.best_p = np; s.best_q = nq; }
-            else if (np == s.best_p) s.best_q = wadd(s.best_q, nq);
-        } else if ((np == -1) | (np == maxint)) {
-            if (s.best_p == -1) fl &= ~OK;
-        } else if ((s.best_p == -1) | (np < s.best_p)) {
-            s.best_p = np; s.best_q = nq;
-        } else if (np == s.best_p) {
+    if (!(fl & OK)) return;
+    const i32 bp = s.best_p;
+    if (BID) {
+        if (np < bp) {
+            if (bp == -1) fl &= ~OK;        // np < -1 on an empty side
+        } else if (np > bp) {
+            s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
+        } else if (bp == -1) {
+            fl &= ~OK;                      // np == -1 on an empty side
+        } else {
+            s.best_q = wadd(s.best_q, nq);
+        }
+    } else {
+        if (np > bp) {
+            if (bp == -1) {                 // empty side
+                if (np == maxint) fl &= ~OK;
+                else { s.best_p = np; s.best_q = nq; }
+            }
+        } else if (np < bp) {
+            if (np != -1) { s.best_p = np; s.best_q = nq; }
+        } else if (np == -1) {
+            fl &= ~OK;
+        } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
         }
     }
@@ -586,6 +632,28 @@ template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i3
     }
 }
 
+// row writes that keep the register price column in step with field FP
+template <int S> DEV void side_put(Side<S>& s, int R, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32 f5) {
+    st6(s.t, s.scr, R, e, f0, f1, f2, f3, f4, f5);
+    col_set(s.pc, e, f0);
+}
+template <int S> DEV void side_clr(Side<S>& s, int R, int e) {
+    clr6(s.t, s.scr, R, e);
+    col_set(s.pc, e, -1);
+}
+// the side's p == -1 slots (all -1 rows in the FAST variant)
+template <int S> DEV void free_slots(const Book<S>& B, const Side<S>& s, lmask (&free)[S]) {
+#pragma unroll
+    for (int r = 0; r < S; ++r) free[r] = B.vs.m[r] & bal(s.pc[r] == -1);
+}
+
+template <int S> DEV bool no_slot(const lmask (&m)[S]) {
+    lmask a = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) a |= m[r];
+    return a == 0ull;
+}
+
 // match_order — JaxOrderBookArrays.py:172-220
 // (qt, pt, ot, tt): the top slot's quantity, price, order id, trader id;
 // tr4: the trade log's OID column
@@ -601,7 +669,7 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
     const int e = first_slot(fm, B.c.nT - 1);
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
-        if (newq <= 0) clr6(s.t, s.scr, R, top);
+        if (newq <= 0) side_clr(s, R, top);
         else stu(s.t, s.scr, R, FQ, top, newq);
         note_reduce<ASKS>(s, B.fl, pt, wsub(qt, newq));
     } else {
@@ -618,15 +686,26 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
 template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     const int R = B.c.nO;
     while (qtm > 0) {
-        if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
-        const i32 mp = BID ? s.best_p : (s.best_p == -1 ? B.c.maxint : s.best_p);
-        if (BID ? !(mp >= price) : !(mp <= price)) break;
-        i32 p[S], q[S], o[S], t[S], ts[S], tn[S], tr4[S];
-        ldcol(s.t, R, FP, p); ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
+        if ((fresh(B.fl) & SideBits<!BID>::OK) == 0u) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+        // the side's best; an empty ask side (-1) counts as maxint (_get_top_ask_order_idx).
+        // BID: `s` is the bid side (an incoming sell crosses when best bid >= price)
+        i32 mp = fresh(s.best_p);
+        if (!BID) {
+            if (mp == -1) {
+                if (fresh(price) != B.c.maxint) break;
+                mp = B.c.maxint;
+            } else if (mp > price) {
+                break;
+            }
+        } else if (mp < price) {
+            break;
+        }
+        i32 q[S], o[S], t[S], ts[S], tn[S], tr4[S];
+        ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
         ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
         ldcol(B.tr.t, B.tr.R, 4, tr4);
-        const int top = top_idx(p, ts, tn, B.vs, B.c, mp);
-        const i32 tp = sget(p, top);
+        const int top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
+        const i32 tp = sget(s.pc, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
         qtm = match_order<G, !BID>(B, s, top, qtm, m, sget(q, top), tp, sget(o, top), sget(t, top), tr4);
     }
@@ -634,15 +713,31 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
 }
 
 // add_order — :62-83 (first slot holding ANY -1 field; none -> last slot)
-// p, q: the side's price and quantity columns, free: its p == -1 slots (from the caller)
+// free: the side's p == -1 slots (from the caller)
 template <bool BID, bool G, int S>
-DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)[S], const i32 (&q)[S],
-                   const lmask (&free)[S]) {
+DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
+    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK,
+                  PM1 = SideBits<!BID>::PM1;
+    const i32 nq = imax_(0, qty);
+    if (!G) {  // FAST: "any -1" <=> p == -1 <=> an all -1 row; no free slot -> the last slot, which holds an order
+        const int e = first_slot(free, R - 1);
+        const bool was_empty = !no_slot(free);
+        if (nq > 0) {
+            side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+            if (m.h & (H_NEG1 | H_PM1)) B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
+            if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
+            else B.fl &= ~OK;
+        } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
+            side_clr(s, R, e);
+            B.fl &= ~OK;
+        }
+        return;
+    }
     lmask fm[S];
-    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK;
-    const bool fast = !G || ((B.fl & (CLEAN | NEG1)) == CLEAN);  // then "any -1" <=> p == -1
-    if (fast) {
+    i32 q[S];
+    ldcol(s.t, R, FQ, q);
+    if ((B.fl & (CLEAN | NEG1 | PM1)) == CLEAN) {  // then "any -1" <=> p == -1
 #pragma unroll
         for (int r = 0; r < S; ++r) fm[r] = free[r];
     } else {
@@ -651,90 +746,67 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const i32 (&p)
         ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
 #pragma unroll
         for (int r = 0; r < S; ++r)
-            fm[r] = B.vs.m[r] & (bal(p[r] == -1) | bal(q[r] == -1) | bal(o[r] == -1) | bal(t[r] == -1) |
+            fm[r] = B.vs.m[r] & (bal(s.pc[r] == -1) | bal(q[r] == -1) | bal(o[r] == -1) | bal(t[r] == -1) |
                                  bal(ts[r] == -1) | bal(tn[r] == -1));
     }
     const int e = first_slot(fm, R - 1);
-    const i32 nq = imax_(0, qty);
-    if (G && !(B.fl & CLEAN)) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
-        st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+    if (!(B.fl & CLEAN)) {  // stray q<=0 rows: write, then the full _removeZeroNegQuant
+        side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        if (m.h & H_PM1) B.fl |= PM1;
         rzn<!BID>(s, B.fl, R, B.vs);
         return;
     }
-    const i32 op = sget(p, e), oq = sget(q, e);
+    const i32 op = sget(s.pc, e), oq = sget(q, e);
     const bool was_empty = (op == -1) & (oq == -1);  // clean: q == -1 <=> all -1 row
     if (nq > 0) {
-        st6(s.t, s.scr, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-        if (m.h & H_NEG1) B.fl = (B.fl | NEG1) & ~F_FAST;
+        side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
+        if (m.h & H_NEG1) B.fl |= NEG1;
+        if (m.h & H_PM1) B.fl |= PM1;
         if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
         else B.fl &= ~OK;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
-        clr6(s.t, s.scr, R, e);
+        side_clr(s, R, e);
         B.fl &= ~OK;
     }
 }
 
 // check_book_fill eviction — :395-401 (bid: worst = min), :484-490 (ask: max);
-// p is the side's price column, reloaded here if rows were cleared
-template <bool BID, int S>
-DEV void evict_worst(Book<S>& B, Side<S>& s, i32 (&p)[S], i32 (&q)[S], lmask (&free)[S]) {
+// called when no slot holds p == -1: evicts only if every price is >= 0
+template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask (&free)[S]) {
     const int R = B.c.nO;
+    lmask neg = 0;
+#pragma unroll
+    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(s.pc[r] < 0);
+    if (neg != 0ull) return;
     i32 w = BID ? INT_MAX : INT_MIN;
 #pragma unroll
     for (int r = 0; r < S; ++r)
-        w = BID ? imin_(w, B.vs.v[r] ? p[r] : INT_MAX) : imax_(w, B.vs.v[r] ? p[r] : INT_MIN);
+        w = BID ? imin_(w, B.vs.v[r] ? s.pc[r] : INT_MAX) : imax_(w, B.vs.v[r] ? s.pc[r] : INT_MIN);
     const i32 worst = BID ? wave_min(w) : wave_max(w);
     lmask m[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(p[r] == worst);
-    clear_masked(s.t, R, m);
+    for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(s.pc[r] == worst);
+    clear_masked(s, R, m);
     B.fl &= ~SideBits<!BID>::OK;
-    ldcol(s.t, R, FP, p);
-    ldcol(s.t, R, FQ, q);
-#pragma unroll
-    for (int r = 0; r < S; ++r) free[r] = B.vs.m[r] & bal(p[r] == -1);
-}
-
-// (called when no slot holds p == -1; `free` is then recomputed after a clear)
-template <bool BID, int S>
-DEV void evict_if_full(Book<S>& B, Side<S>& s, i32 (&p)[S], i32 (&q)[S], lmask (&free)[S]) {
-    lmask neg = 0;
-#pragma unroll
-    for (int r = 0; r < S; ++r) neg |= B.vs.m[r] & bal(p[r] < 0);
-    if (neg == 0ull) evict_worst<BID>(B, s, p, q, free);
-}
-// the side's price / quantity columns and its p == -1 slots
-template <int S> DEV void load_pq_free(const Book<S>& B, const Side<S>& s, i32 (&p)[S], i32 (&q)[S], lmask (&free)[S]) {
-    ldcol(s.t, B.c.nO, FP, p);
-    ldcol(s.t, B.c.nO, FQ, q);
-#pragma unroll
-    for (int r = 0; r < S; ++r) free[r] = B.vs.m[r] & bal(p[r] == -1);
-}
-template <int S> DEV bool no_slot(const lmask (&m)[S]) {
-    lmask a = 0;
-#pragma unroll
-    for (int r = 0; r < S; ++r) a |= m[r];
-    return a == 0ull;
+    free_slots(B, s, free);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
     if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
-    i32 p[S], q[S];
     lmask free[S];
-    load_pq_free(B, B.b, p, q, free);
-    if (B.c.check_fill && no_slot(free)) evict_if_full<true>(B, B.b, p, q, free);
-    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, p, q, free);
+    free_slots(B, B.b, free);
+    if (B.c.check_fill && no_slot(free)) evict_if_full<true>(B, B.b, free);
+    if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
 }
 // ask_lim — :446-508
 template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (B.c.t4 == 2) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
-    i32 p[S], q[S];
     lmask free[S];
-    load_pq_free(B, B.a, p, q, free);
-    if (B.c.check_fill && no_slot(free)) evict_if_full<false>(B, B.a, p, q, free);
-    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, p, q, free);
+    free_slots(B, B.a, free);
+    if (B.c.check_fill && no_slot(free)) evict_if_full<false>(B, B.a, free);
+    if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, free);
 }
 // get_random_id_match / get_random_large_id_match — :141-164 (cancel_mode 2/3).
 // key = split(key)[0]; chosen = jax.random.choice(key, ids, p=|sign(ids)|),
@@ -782,9 +854,8 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
     // unused cancel rows (getCancelMsgs' zero rows) are such messages.
     if (!G && m.qty == 0) return;
     const int R = B.c.nO;
-    i32 o[S], p[S], q[S];
+    i32 o[S], q[S];
     ldcol(s.t, R, FOID, o);
-    ldcol(s.t, R, FP, p);
     ldcol(s.t, R, FQ, q);
     lmask fm[S];
 #pragma unroll
@@ -794,7 +865,7 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
         const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
 #pragma unroll
         for (int r = 0; r < S; ++r)
-            fm[r] = B.vs.m[r] & bal(p[r] == m.price) & bal(o[r] <= B.c.init_id) & bal(o[r] >= lo) &
+            fm[r] = B.vs.m[r] & bal(s.pc[r] == m.price) & bal(o[r] <= B.c.init_id) & bal(o[r] >= lo) &
                     bal(q[r] >= m.qty);
         if (!RC) {
             idx = first_slot(fm, R - 1);  // -1 wraps to the last slot
@@ -803,21 +874,21 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
             if (idx < 0 && B.c.cancel_mode >= 2) {
                 Key k = split_key(B.ek, B.nmsg, B.mi, B.part);
 #pragma unroll
-                for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == m.price) & bal(q[r] >= m.qty);
+                for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(s.pc[r] == m.price) & bal(q[r] >= m.qty);
                 idx = random_id_match(B, k, o, fm);
                 if (idx < 0 && B.c.cancel_mode == 3) {
 #pragma unroll
-                    for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(p[r] == m.price);
+                    for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(s.pc[r] == m.price);
                     idx = random_id_match(B, k, o, fm);
                 }
             }
             if (idx < 0) idx = R - 1;
         }
     }
-    const i32 op = sget(p, idx), oq = sget(q, idx);
+    const i32 op = sget(s.pc, idx), oq = sget(q, idx);
     const i32 nq = wsub(oq, m.qty);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
-        if (nq <= 0) clr6(s.t, s.scr, R, idx);
+        if (nq <= 0) side_clr(s, R, idx);
         else stu(s.t, s.scr, R, FQ, idx, nq);
         note_reduce<ASKS>(s, B.fl, op, wsub(oq, nq > 0 ? nq : 0));
     } else {
@@ -834,7 +905,8 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
 // H_DISCARD: a type-4 message under type_4_interpretation 0/2 is not added
 // after matching.  H_NEG1: the row add_order would write has p != -1 and a -1
 // in another field (it sets the side's NEG1 flag); the price it writes is the
-// message's, or maxint / 0 for MKT bids / asks.
+// message's, or maxint / 0 for MKT bids / asks.  H_PM1: that price is -1 (the
+// row would be an order priced -1: the side's PM1 flag).
 DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     const i32 ty = x.x, sd = ty == 4 ? wsub(0, x.y) : x.y;
     const bool cnl = (ty == 2) | (ty == 3);
@@ -846,6 +918,7 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     if (((c.t4 == 0) | (c.t4 == 2)) & (ty == 4)) h |= H_DISCARD;
     const i32 p_add = c.t4 == 2 ? (h == H_BID ? c.maxint : 0) : x.w;
     if ((p_add != -1) & ((y.x == -1) | (y.y == -1) | (y.z == -1) | (y.w == -1))) h |= H_NEG1;
+    if (p_add == -1) h |= H_PM1;  // an add would write an order priced -1
     x.x = h;
     x.y = sd;
 }
@@ -977,10 +1050,9 @@ template <int S> DEV i32 side_volume_pq(const i32 (&p)[S], const i32 (&q)[S], co
     return wave_sum(v);
 }
 template <int S> DEV i32 side_volume(const Side<S>& s, int R, const Valid<S>& V) {
-    i32 p[S], q[S];
-    ldcol(s.t, R, FP, p);
+    i32 q[S];
     ldcol(s.t, R, FQ, q);
-    return side_volume_pq(p, q, V);
+    return side_volume_pq(s.pc, q, V);
 }
 // prices and quantities of a global [R][6] side, lane-strided into registers
 template <int S> DEV void global_pq(const i32* g, const Valid<S>& V, i32 (&p)[S], i32 (&q)[S]) {
@@ -1249,10 +1321,10 @@ template <int S>
 DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int size, i32 side, i32 t, i32 tns,
                      i32* lds_rows, int row0) {
     int n = 0;
-    i32 tid[S], q[S], p[S], o[S];  // one LDS round trip; hit rows are read from registers
+    i32 tid[S], q[S], o[S];  // one LDS round trip; hit rows are read from registers
+    const i32 (&p)[S] = s.pc;
     ldcol(s.t, R, FTID, tid);
     ldcol(s.t, R, FQ, q);
-    ldcol(s.t, R, FP, p);
     ldcol(s.t, R, FOID, o);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
@@ -1318,9 +1390,11 @@ DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
 template <int S>
 DEV bool masked_best(const hftlob_env_cfg& c, Book<S>& B, i32 tid, i32 last_ba, i32 last_bb, i32& ba, i32& bb) {
     const i32 tick = c.tick_size;
-    i32 mn = INT_MAX, mx = INT_MIN, ap_[S], at_[S], bp_[S], bt_[S];
-    ldcol(B.a.t, B.c.nO, FP, ap_); ldcol(B.a.t, B.c.nO, FTID, at_);
-    ldcol(B.b.t, B.c.nO, FP, bp_); ldcol(B.b.t, B.c.nO, FTID, bt_);
+    i32 mn = INT_MAX, mx = INT_MIN, at_[S], bt_[S];
+    const i32 (&ap_)[S] = B.a.pc;
+    const i32 (&bp_)[S] = B.b.pc;
+    ldcol(B.a.t, B.c.nO, FTID, at_);
+    ldcol(B.b.t, B.c.nO, FTID, bt_);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
         const i32 pa = (B.vs.v[r] && at_[r] != tid) ? ap_[r] : -1;

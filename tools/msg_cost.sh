@@ -9,7 +9,7 @@ P2="SQ_WAVES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_ACTIV
 P3="SQ_WAVES SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/mc_$T/p0 -o mc -- python $GRAFT_REPO_ROOT/tools/msg_cost.py > $O/mc_$T.log 2>&1 || exit 1
 i=0
-for P in "$P1" "$P2" "$P3"; do
+for P in "$P1"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $O/mc_$T/p$i -o mc -- python $GRAFT_REPO_ROOT/tools/msg_cost.py > $O/mc_$T.log 2>&1 || exit 1
 done
