@@ -686,13 +686,13 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
 template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     const int R = B.c.nO;
     while (qtm > 0) {
-        if ((fresh(B.fl) & SideBits<!BID>::OK) == 0u) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+        if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
         // the side's best; an empty ask side (-1) counts as maxint (_get_top_ask_order_idx).
         // BID: `s` is the bid side (an incoming sell crosses when best bid >= price)
-        i32 mp = fresh(s.best_p);
+        i32 mp = s.best_p;
         if (!BID) {
             if (mp == -1) {
-                if (fresh(price) != B.c.maxint) break;
+                if (price != B.c.maxint) break;
                 mp = B.c.maxint;
             } else if (mp > price) {
                 break;
@@ -790,22 +790,52 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
     B.fl &= ~SideBits<!BID>::OK;
     free_slots(B, s, free);
 }
+// The common add: FAST book, a free (all -1) slot exists, no eviction: the order goes to the
+// first free slot (add_order's "first row holding any -1").  Flag changes are rare (orders with
+// -1 fields), so they stay behind a branch.
+template <bool BID, int S> DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
+    const int R = B.c.nO;
+    if (qty <= 0) return;  // imax(0, qty) == 0: the new row is removed at once and the slot was empty
+    u32 e = ff1(free[0]);
+#pragma unroll
+    for (int r = 1; r < S; ++r) e = min(e, ff1(free[r]) | (u32)(64 * r));
+    side_put(s, R, (int)e, m.price, qty, m.oid, m.tid, m.t, m.tns);
+    if (__builtin_expect((m.h & (H_NEG1 | H_PM1)) != 0, 0)) {
+        constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
+        B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
+    }
+    note_add<BID>(s, B.fl, m.price, qty, B.c.maxint);
+}
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
-    if (B.c.t4 == 2) m.price = B.c.maxint;  // MKT: set after matching (sic)
+    if (__builtin_expect(B.c.t4 == 2, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
     lmask free[S];
     free_slots(B, B.b, free);
-    if (B.c.check_fill && no_slot(free)) evict_if_full<true>(B, B.b, free);
+    if (!no_slot(free)) {
+        if (!(m.h & H_DISCARD)) {
+            if (!G) add_free<true>(B, B.b, m, rem, free);
+            else add_order<true, G>(B, B.b, m, rem, free);
+        }
+        return;
+    }
+    if (B.c.check_fill) evict_if_full<true>(B, B.b, free);
     if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
 }
 // ask_lim — :446-508
 template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
-    if (B.c.t4 == 2) m.price = 0;
+    if (__builtin_expect(B.c.t4 == 2, 0)) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
     lmask free[S];
     free_slots(B, B.a, free);
-    if (B.c.check_fill && no_slot(free)) evict_if_full<false>(B, B.a, free);
+    if (!no_slot(free)) {
+        if (!(m.h & H_DISCARD)) {
+            if (!G) add_free<false>(B, B.a, m, rem, free);
+            else add_order<false, G>(B, B.a, m, rem, free);
+        }
+        return;
+    }
+    if (B.c.check_fill) evict_if_full<false>(B, B.a, free);
     if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, free);
 }
 // get_random_id_match / get_random_large_id_match — :141-164 (cancel_mode 2/3).
@@ -862,11 +892,19 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
     for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
     int idx = first_slot(fm, -1);
     if (idx < 0) {
+        // get_init_id_match: price == msg price, init_id - 2 * depth <= oid <= init_id, q >= msg q.
+        // Evaluated per lane in VALU (selects feeding one compare), not as three lane masks ANDed on
+        // the scalar unit: oid in range <=> (u32)(oid - lo) <= (u32)(init_id - lo), given lo <= init_id
+        // (check_lob refuses book_depth < 0 and an overflowing init_id - 2 * book_depth).
         const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
+        const u32 span = (u32)wsub(B.c.init_id, lo);
 #pragma unroll
-        for (int r = 0; r < S; ++r)
-            fm[r] = B.vs.m[r] & bal(s.pc[r] == m.price) & bal(o[r] <= B.c.init_id) & bal(o[r] >= lo) &
-                    bal(q[r] >= m.qty);
+        for (int r = 0; r < S; ++r) {
+            u32 d = (u32)wsub(o[r], lo);
+            d = s.pc[r] == m.price ? d : 0xFFFFFFFFu;
+            d = q[r] >= m.qty ? d : 0xFFFFFFFFu;
+            fm[r] = B.vs.m[r] & bal(d <= span);
+        }
         if (!RC) {
             idx = first_slot(fm, R - 1);  // -1 wraps to the last slot
         } else {
@@ -2554,6 +2592,9 @@ static int check_lob(const hftlob_lob_cfg* c) {
     if (c->type_4_interpretation < 0 || c->type_4_interpretation > 2) return fail(HFTLOB_EINVAL, "bad type_4_interpretation");
     if (c->n_orders < 1 || c->n_orders > HFTLOB_MAX_SLOTS || c->n_trades < 1 || c->n_trades > HFTLOB_MAX_SLOTS)
         return fail(HFTLOB_ESHAPE, "n_orders / n_trades out of range");
+    // get_init_id_match's id range [init_id - 2 * book_depth, init_id] must be a plain int32 range
+    if (c->book_depth < 0 || (long long)c->init_id - 2LL * c->book_depth < INT_MIN)
+        return fail(HFTLOB_EINVAL, "book_depth must be >= 0 and init_id - 2 * book_depth must fit in int32");
     return HFTLOB_OK;
 }
 static int launch_status() {

@@ -296,6 +296,9 @@ def pack_lob_cfg(w, prng_partitionable: bool = True) -> LobCfg:
         raise NotImplementedError("simulator_mode LOBSTER_INTERPRETER is not implemented (reference: NotImplementedError)")
     if w.cancel_mode not in (0, 1, 2, 3):
         raise ValueError(f"cancel_mode {w.cancel_mode} (jaxob_constants.CancelMode has 0..3)")
+    if w.book_depth < 0 or w.init_id - 2 * w.book_depth < -2**31:
+        raise ValueError("book_depth must be >= 0 and init_id - 2 * book_depth must fit in int32 "
+                         "(the init-order id range of get_init_id_match, JaxOrderBookArrays.py:120-139)")
     c = LobCfg()
     c.maxint, c.init_id, c.book_depth = w.maxint, w.init_id, w.book_depth
     c.cancel_mode, c.type_4_interpretation = w.cancel_mode, w.type_4_interpretation
