@@ -569,6 +569,10 @@ struct Book {
     // of the message being processed (keys = split(ek, nmsg); key i is message i's)
     Key ek;
     i32 mi, nmsg;
+    // trade log: rows [0, ntr) hold col 4 != -1, rows [ntr, nT) col 4 == -1, so the next trade
+    // goes to row min(ntr, nT - 1) (match_order's "first row whose col 4 == -1", -1 -> last row).
+    // -1: the log loaded from memory has no such prefix shape; match_order then searches it.
+    i32 ntr;
     bool part;
 };
 
@@ -658,15 +662,22 @@ template <int S> DEV bool no_slot(const lmask (&m)[S]) {
 // (qt, pt, ot, tt): the top slot's quantity, price, order id, trader id;
 // tr4: the trade log's OID column
 template <bool G, bool ASKS, int S>
-DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 qt, i32 pt, i32 ot, i32 tt,
-                    const i32 (&tr4)[S]) {
+DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 qt, i32 pt, i32 ot, i32 tt) {
     const int R = B.c.nO;
     const i32 newq = imax_(0, wsub(qt, qtm));
     const i32 rem = wsub(qtm, qt);
-    lmask fm[S];
+    int e;
+    if (B.ntr >= 0) {  // the row after the last written one; a trade with col 4 (aggressor oid) == -1 leaves it free
+        e = imin_(B.ntr, B.c.nT - 1);
+        if (m.oid != -1) B.ntr = imin_(B.ntr + 1, B.c.nT);
+    } else {
+        i32 tr4[S];
+        ldcol(B.tr.t, B.tr.R, 4, tr4);
+        lmask fm[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(tr4[r] == -1);  // trade[:,OID=4] == -1
-    const int e = first_slot(fm, B.c.nT - 1);
+        for (int r = 0; r < S; ++r) fm[r] = B.vt.m[r] & bal(tr4[r] == -1);  // trade[:,OID=4] == -1
+        e = first_slot(fm, B.c.nT - 1);
+    }
     trade_put(B.tr, e, pt, wmul(wsub(0, m.side), wsub(qt, newq)), ot, m.oid, m.t, m.tns, tt, m.tid);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (newq <= 0) side_clr(s, R, top);
@@ -700,14 +711,13 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
         } else if (mp < price) {
             break;
         }
-        i32 q[S], o[S], t[S], ts[S], tn[S], tr4[S];
+        i32 q[S], o[S], t[S], ts[S], tn[S];
         ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
         ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
-        ldcol(B.tr.t, B.tr.R, 4, tr4);
         const int top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
         const i32 tp = sget(s.pc, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
-        qtm = match_order<G, !BID>(B, s, top, qtm, m, sget(q, top), tp, sget(o, top), sget(t, top), tr4);
+        qtm = match_order<G, !BID>(B, s, top, qtm, m, sget(q, top), tp, sget(o, top), sget(t, top));
     }
     return qtm;
 }
@@ -1026,6 +1036,16 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs);
     B.fl |= fast_bit(B.fl);
     load_trades(B.tr, gt, B.vt);
+    {  // the loaded log's free-row prefix (see Book::ntr)
+        lmask fr[S], bad = 0;
+#pragma unroll
+        for (int r = 0; r < S; ++r) fr[r] = B.vt.m[r] & bal(B.tr.get(4, r) == -1);
+        const int first = first_slot(fr, B.c.nT);
+        const int l = lane_id();
+#pragma unroll
+        for (int r = 0; r < S; ++r) bad |= B.vt.m[r] & ~fr[r] & bal(r * 64 + l >= first);
+        B.ntr = bad == 0ull ? first : -1;
+    }
     if (RC) {
         B.ek = Key{keys[2 * e], keys[2 * e + 1]};
         B.nmsg = n_msg;
@@ -2290,6 +2310,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     STAMP(t_agents);
     // ---- (B)+(D) stream the combined messages through the book, 64 per chunk
     trades_fill(B.tr, B.vt, -1);
+    B.ntr = 0;
     const int AR = C + A;
     bool abort_any = false;
     i32 prev_a = -1, prev_b = -1;
