@@ -119,6 +119,19 @@ DEV i32 fresh(i32 v) {
     asm volatile("" : "+s"(v));
     return v;
 }
+// c ? a : b on two fields of a local struct, kept a select of VALUES: the compiler turns
+// "select of two loads" into a load through a selected address, which puts the whole struct
+// in scratch memory (64 lanes x its size of extra memory traffic per use)
+DEV i32 sel(bool c, i32 a, i32 b) {
+    asm volatile("" : "+v"(a));
+    asm volatile("" : "+v"(b));
+    return c ? a : b;
+}
+DEV float self(bool c, float a, float b) {  // (uniform floats live in VGPRs: the VALU computes them)
+    asm volatile("" : "+v"(a));
+    asm volatile("" : "+v"(b));
+    return c ? a : b;
+}
 
 // Diagnostic build only (-DHFTLOB_STAMPS): per-phase shader-clock stamps of
 // k_env_step, written to the info buffer in place of the info fields.
@@ -1134,8 +1147,18 @@ template <int S> DEV float rows_fsum(const float (&x)[S], int n) {
     return wave_fsum(a);
 }
 
-struct Obs {
-    float v[HFTLOB_MAX_OBS];
+// One agent's observation row, one field per lane: `o[k] = x` keeps x in lane k.  (The obs
+// functions fill fields by config-dependent branches; a local float array written that way
+// ends up in scratch memory, with a scratch store per field per lane.)
+struct ObsLane {
+    int l;
+    float v;
+    struct Ref {
+        ObsLane& o;
+        int k;
+        DEV void operator=(float x) { o.v = o.l == k ? x : o.v; }
+    };
+    DEV Ref operator[](int k) { return Ref{*this, k}; }
 };
 
 struct WorldView {  // wave-uniform world quantities used by obs
@@ -1147,7 +1170,7 @@ struct WorldView {  // wave-uniform world quantities used by obs
 };
 
 // MM _get_obs_basic / _get_obs_engineered (fixed_steps), sorted keys — mm_env.py:2963-3154
-DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o,
+DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, ObsLane& o,
                 bool ftime) {
     const bool nz = tc.normalize;
     const i32 spread = iabs_(wsub(w.best_ask_p, w.best_bid_p));
@@ -1183,7 +1206,7 @@ DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const 
 }
 // EXE _get_obs (fixed_steps), sorted keys — exec_env.py:1913-2079
 // ftime: ep_type == fixed_time, passed by the caller (compile-time false in the 100/100 kernel)
-DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, float* o,
+DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, ObsLane& o,
                  bool ftime) {
     const bool nz = tc.normalize;
     if (tc.observation_space == HFTLOB_EXE_OBS_BASIC) {  // :1879-1911 best_ask_price, best_bid_price, remaining_quant
@@ -1262,16 +1285,11 @@ DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
 // write one agent's obs row (lanes 0..obs_stride-1 store one float each)
 DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st,
                    float* dst, bool zero, bool ftime) {
-    float o[HFTLOB_MAX_OBS];
-#pragma unroll
-    for (int k = 0; k < HFTLOB_MAX_OBS; ++k) o[k] = 0.0f;
+    const int l = lane_id();
+    ObsLane o{l, 0.0f};
     if (tc.kind == HFTLOB_AGENT_MM) mm_obs(c, tc, w, st, o, ftime);
     else exe_obs(c, tc, w, st, o, ftime);
-    const int l = lane_id();
-    float v = 0.0f;
-#pragma unroll
-    for (int k = 0; k < HFTLOB_MAX_OBS; ++k) if (l == k) v = o[k];
-    if (zero) v = 0.0f;
+    const float v = zero ? 0.0f : o.v;
     if (l < c.obs_stride) dst[l] = v;
 }
 
@@ -1492,8 +1510,11 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
         const int ai = action < 0 ? imax_(action + 9, 0) : (action > 8 ? 8 : action);
         const i32 bot[9] = {10, 2, 4, -1, 0, 2, -20, 0, 0}, aot[9] = {10, 2, 4, -1, 2, 0, 0, -20, 0};
         const i32 iq = ifloordiv(st[2], tc.fixed_quant_value);
-        bo = i2f(bot[ai]);
-        ao = i2f(aot[ai]);
+        i32 b = bot[0], a = aot[0];  // table lookups as selects: a dynamically indexed local array lives in scratch
+#pragma unroll
+        for (int k = 1; k < 9; ++k) { b = ai == k ? bot[k] : b; a = ai == k ? aot[k] : a; }
+        bo = i2f(b);
+        ao = i2f(a);
         bq = wmul(ai < 6 ? 1 : (ai == 6 ? iq : 0), tc.fixed_quant_value);
         aq = wmul(ai < 6 ? 1 : (ai == 7 ? iq : 0), tc.fixed_quant_value);
     }
@@ -1654,7 +1675,9 @@ DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
         // quant table rows: action 0 -> none; 1..12 -> level (ai-1)%4 with multiple {1,2,5}[(ai-1)/4]
         if (ai > 0) {
             const int lvl = (ai - 1) & 3, mul = (ai - 1) >> 2;
-            q[lvl] = wmul(mul == 0 ? 1 : (mul == 1 ? 2 : 5), fq);
+            const i32 v = wmul(mul == 0 ? 1 : (mul == 1 ? 2 : 5), fq);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = k == lvl ? v : 0;  // (selects: no dynamically indexed array)
         }
         const i32 tot = wadd(wadd(q[0], q[1]), wadd(q[2], q[3]));
         if (!(tot <= left)) { q[0] = f2i(floorf(i2f(left))); q[1] = q[2] = q[3] = 0; }
@@ -1663,7 +1686,9 @@ DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
     }
     if (tc.action_space == HFTLOB_EXE_ACT_FIXED_QUANTS_1MSG) {  // one row at [0, FT, M, NT, PP][a]
         const int ai = action < 0 ? imax_(action + 5, 0) : (action > 4 ? 4 : action);
-        const i32 p = ai == 0 ? 0 : pl[ai - 1];
+        i32 p = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p = ai == k + 1 ? pl[k] : p;
         i32 qq = ai == 0 ? 0 : fq;
         qq = qq <= left ? qq : 0;
         put_row(lds_rows, row, 1, side, qq, p, c.placeholder_order_id, tid, ta, tb);
@@ -1809,8 +1834,8 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     i32 pen = wmul(tc.unwind_price_penalty, c.tick_size);
     pen = inv_b > 0 ? pen : wsub(0, pen);
     i32 unwind_px;
-    if (tc.unwind_price == HFTLOB_PRICE_FAR_TOUCH) unwind_px = wsub(inv_b > 0 ? X.last_bb : X.last_ba, pen);
-    else unwind_px = f2i((tc.unwind_price == HFTLOB_PRICE_MID_AVG ? X.avg_mid : X.last_mid) - i2f(pen));
+    if (tc.unwind_price == HFTLOB_PRICE_FAR_TOUCH) unwind_px = wsub(sel(inv_b > 0, X.last_bb, X.last_ba), pen);
+    else unwind_px = f2i(self(tc.unwind_price == HFTLOB_PRICE_MID_AVG, X.avg_mid, X.last_mid) - i2f(pen));
     const bool add = X.ep_done && iabs_(inv_b) > 0;
     const i32 ovr[8] = {unwind_px, wmul(isign(inv_b), iabs_(inv_b)), c.artificial_order_id, c.placeholder_order_id,
                         0, 0, c.artificial_trader_id, tid};
@@ -1850,8 +1875,8 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     if (ri == HFTLOB_PRICE_MID_AVG) { ref_buy = ref_sell = ref = X.avg_mid; }
     else if (ref_int) {
         const bool far = ri == HFTLOB_PRICE_FAR_TOUCH;
-        rbi = far ? X.last_ba : X.last_bb;
-        rsi = far ? X.last_bb : X.last_ba;
+        rbi = sel(far, X.last_ba, X.last_bb);
+        rsi = sel(far, X.last_bb, X.last_ba);
         refi = new_inv > 0 ? rbi : rsi;
         ref_buy = i2f(rbi); ref_sell = i2f(rsi); ref = i2f(refi);
     } else { ref_buy = ref_sell = ref = X.last_mid; }
@@ -1899,8 +1924,8 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     }
     const float r_pv = i2f(new_inv) * (ref / tick) + cash;
     float old_ref;
-    if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(inv > 0 ? X.old_last_ba : X.old_last_bb);
-    else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(inv > 0 ? X.old_last_bb : X.old_last_ba);
+    if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_ba, X.old_last_bb));
+    else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_bb, X.old_last_ba));
     else old_ref = X.wmid;
     const float old_nw = old_ref / tick * i2f(inv) + bitf(st[4]);
     const float d_nw = net_worth - old_nw;
@@ -2063,13 +2088,13 @@ DEV Key from_lane(Key v, int src) {  // per-lane gather v[src]
     return Key{(u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.a), (u32)__builtin_amdgcn_ds_bpermute(src << 2, (i32)v.b)};
 }
 template <bool MD>  // MD: the config may hold MultiDiscrete (fixed_prices) agent types
-DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* keys, const Key* master) {
+DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* keys, bool sampled, const Key& master) {
     const bool part = c.prng_partitionable;
     const int l = lane_id(), nTy = c.n_types, A = c.n_action_msgs;
     Key key;
     Key nm{0u, 0u};
-    if (master) {  // lane 0: this env's key; lane 1: the carried master key
-        const Key v = split_key(*master, n_env + 1, l == 0 ? e + 1 : 0, part);
+    if (sampled) {  // lane 0: this env's key; lane 1: the carried master key
+        const Key v = split_key(master, n_env + 1, l == 0 ? e + 1 : 0, part);
         key = lane_key(v);
         nm = Key{(u32)rdl((i32)v.a, 1), (u32)rdl((i32)v.b, 1)};
     } else {
@@ -2121,13 +2146,14 @@ DEV void fixed_time_mask(int4& x, int4& y, i32 t_end) {
 // 100/100 default), which folds the slot-validity masks away.
 template <int S, int NFIX, bool RC>
 // RC: cancel_mode 2/3 (the random cancel fallback of the engine).
-// master != NULL: Speed_test rollout mode — the env's step key is
-// split(*master, n_env + 1)[e + 1], actions are sampled here (hftlob_sample_actions)
-// and written to actions_io if it is not NULL; *master becomes split(*master)[0].
-// Otherwise keys / actions_io are the inputs.
+// master: Speed_test rollout mode — the env's step key is split(mk, n_env + 1)[e + 1],
+// actions are sampled here (hftlob_sample_actions) and written to actions_io if it is not
+// NULL; mk becomes split(mk)[0].  Otherwise keys / actions_io are the inputs.  (mk is a
+// reference, not a pointer: an address-taken local would live in scratch memory.)
 // key_n / ek: the env count of the step-key split and this env's index in it;
 // e: this env's record / output index
-DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u32* __restrict__ keys, Key* master,
+DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u32* __restrict__ keys, bool master,
+                      Key& mk,
                       i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
                       const i32* __restrict__ init_states, i32* __restrict__ state, float* __restrict__ obs_out,
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
@@ -2147,8 +2173,8 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
     fetch_side(fa, rec + c.off_asks, B.vs);
     fetch_side(fb, rec + c.off_bids, B.vs);
-    const StepKeys SK = step_keys<NFIX == 0>(c, key_n, ek, keys, master);
-    if (master) *master = SK.next_master;
+    const StepKeys SK = step_keys<NFIX == 0>(c, key_n, ek, keys, master, mk);
+    if (master) mk = SK.next_master;
     const Key key_reset = SK.key_reset;
     if (RC) {  // the scan's key: k1, or split(k1)[0] after the shuffle split (marl_env.py:293-294,349-351)
         B.ek = c.shuffle_action_messages ? split_key(SK.k1, 2, 0, c.prng_partitionable) : SK.k1;
@@ -2517,7 +2543,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
     if (e >= n_env) return;
     Key mk{0u, 0u};
     if (master) mk = Key{master[0], master[1]};
-    env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master ? &mk : nullptr, actions_io, msg_data, init_states,
+    env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master != nullptr, mk, actions_io, msg_data, init_states,
                               state, obs_out, rew_out, done_all_out, dones_out, info_out, lds);
     if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
@@ -2557,7 +2583,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         const i32* is = init_states;
         asm volatile("" : "+s"(cp), "+s"(st), "+s"(md), "+s"(is));
         const hftlob_env_cfg& cc = *(const hftlob_env_cfg*)cp;
-        env_step_dev<S, NFIX, RC>(cc, key_n, key_e0 + e, e, nullptr, &mk,
+        env_step_dev<S, NFIX, RC>(cc, key_n, key_e0 + e, e, nullptr, true, mk,
                                   actions_io ? actions_io + o * cc.action_words : nullptr, md, is, st,
                                   obs_out + o * cc.n_agents * cc.obs_stride, rew_out + o * cc.n_agents,
                                   done_all_out + o, dones_out + o * cc.n_agents,

@@ -9,10 +9,11 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = "/tmp/libhftlob_stamps.so"
-subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC",
+SO = os.environ.get("HFTLOB_STAMPS_LIB") or "/tmp/libhftlob_stamps.so"
+if not os.path.exists(SO):
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC",
                 "-DHFTLOB_STAMPS", "-mllvm", "-structurizecfg-skip-uniform-regions=true", "-shared", "-o", SO, os.path.join(ROOT, "jaxmarl-hft_amd/csrc/hftlob.hip")],
-               check=True)
+                   check=True)
 os.environ["HFTLOB_LIB"] = SO
 sys.path.insert(0, os.path.join(ROOT, "jaxmarl-hft_amd"))
 import numpy as np  # noqa: E402
