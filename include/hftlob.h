@@ -68,7 +68,7 @@ enum { HFTLOB_AGENT_MM = 0, HFTLOB_AGENT_EXE = 1 };
 enum { HFTLOB_MM_ACT_FIXED_QUANTS = 0, HFTLOB_MM_ACT_DIRECTIONAL = 1, HFTLOB_MM_ACT_BOB_RL = 2,
        HFTLOB_MM_ACT_BOB_STRATEGY = 3, HFTLOB_MM_ACT_AVST = 4, HFTLOB_MM_ACT_SPREAD_SKEW = 5,
        HFTLOB_MM_ACT_SIMPLE = 6 };
-enum { HFTLOB_MM_OBS_BASIC = 0, HFTLOB_MM_OBS_ENGINEERED = 1 };
+enum { HFTLOB_MM_OBS_BASIC = 0, HFTLOB_MM_OBS_ENGINEERED = 1, HFTLOB_MM_OBS_MESSAGES = 2 };
 enum { HFTLOB_MM_REW_PORTFOLIO_VALUE = 0, HFTLOB_MM_REW_BUY_SELL_PNL, HFTLOB_MM_REW_COMPLEX,
        HFTLOB_MM_REW_ZERO_INV, HFTLOB_MM_REW_SPOONER, HFTLOB_MM_REW_SPOONER_DAMPED,
        HFTLOB_MM_REW_SPOONER_ASYM_DAMPED, HFTLOB_MM_REW_SPOONER_ASYM_DAMPED2,
@@ -203,20 +203,32 @@ typedef struct hftlob_env_cfg {
 } hftlob_env_cfg;
 
 /* Outputs of one batched step / reset.  obs/rewards/dones may not be NULL;
- * info may be NULL (skipped).  Layouts:
+ * info, obs_raw and msgs may be NULL (skipped).  Layouts:
  *   obs      f32   [n_env][n_agents][obs_stride]   (agent order = type order)
  *   rewards  f32   [n_env][n_agents]
  *   done_all bool (uint8 0/1) [n_env]              dones["__all__"]
  *   dones    bool (uint8 0/1) [n_env][n_agents]    dones["agents"]
  *   info     32-bit words [n_env][info_words]: world info then one
  *            HFTLOB_INFO_AGENT_WORDS block per agent (ints, or f32 bit-cast;
- *            field map in hftlob/layout.py) */
+ *            field map in hftlob/layout.py)
+ *   obs_raw  32-bit words [n_env][n_agents][obs_stride] (step only): each agent's
+ *            un-normalised observation of the stepped state, the reference's
+ *            info["agents"][t]["obs_raw"] under save_raw_observations
+ *            (marl_env.py:684-685: get_observation(..., normalize=False,
+ *            flatten=False)), fields in sorted-key order, int32 fields as int32 and
+ *            float32 fields as f32 bits (key / dtype map in hftlob/layout.py); not
+ *            zeroed for done agents and taken before the auto-reset, as info is
+ *   msgs     int32 [n_env][n_msgs][8] (step only): the step's combined message
+ *            array [cancels; shuffled actions; data] as processed by the book —
+ *            the MM "messages" observation (mm_env.py:2820-2821) */
 typedef struct hftlob_step_out {
     float*   obs;
     float*   rewards;
     uint8_t* done_all;
     uint8_t* dones;
     int32_t* info;
+    int32_t* obs_raw;
+    int32_t* msgs;
 } hftlob_step_out;
 
 int         hftlob_version(void);

@@ -1159,6 +1159,7 @@ struct ObsLane {
         DEV void operator=(float x) { o.v = o.l == k ? x : o.v; }
     };
     DEV Ref operator[](int k) { return Ref{*this, k}; }
+    DEV void put_i(int k, i32 x) { v = l == k ? __int_as_float(x) : v; }  // an int32 field, kept as its bits
 };
 
 struct WorldView {  // wave-uniform world quantities used by obs
@@ -1169,55 +1170,65 @@ struct WorldView {  // wave-uniform world quantities used by obs
     float dt;
 };
 
-// MM _get_obs_basic / _get_obs_engineered (fixed_steps), sorted keys — mm_env.py:2963-3154
+// MM _get_obs_basic / _get_obs_engineered, sorted keys — mm_env.py:2963-3154.
+// RAW: get_observation(normalize=False, flatten=False) for save_raw_observations
+// (marl_env.py:684-685): no normalisation, and the int32 fields keep their int32
+// value (stored as int bits; flattening is what casts them to float).
+#define OBS_I(k, x, expr) do { if (RAW) o.put_i((k), (x)); else o[k] = (expr); } while (0)
+template <bool RAW>
 DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, ObsLane& o,
                 bool ftime) {
-    const bool nz = tc.normalize;
+    const bool nz = !RAW && tc.normalize;
     const i32 spread = iabs_(wsub(w.best_ask_p, w.best_bid_p));
-    if (tc.observation_space == HFTLOB_MM_OBS_BASIC) {
-        o[0] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
-        o[1] = nz ? i2f(spread) / 1e4f : i2f(spread);
+    if (tc.observation_space == HFTLOB_MM_OBS_BASIC) {  // inventory, spread
+        OBS_I(0, st[2], nz ? i2f(st[2]) / 10.0f : i2f(st[2]));
+        OBS_I(1, spread, nz ? i2f(spread) / 1e4f : i2f(spread));
         return;
     }
+    // "messages" (mm_env.py:2820-2821): the observation is the step's message array, written
+    // by env_step_dev to out.msgs; the float row stays zero
+    if (tc.observation_space == HFTLOB_MM_OBS_MESSAGES) return;
     if (ftime) {  // mm_env.py:3029-3088, sorted keys: delta_time, inventory, mid_price, p_ask, p_bid, q_ask,
                   // q_bid, spread, step_counter, time_remaining
         const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
         const float trem = (float)c.episode_time - (tm - (i2f(w.it0) + i2f(w.it1) / 1e9f));
         o[0] = nz ? w.dt / 10.0f : w.dt;
-        o[1] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
+        OBS_I(1, st[2], nz ? i2f(st[2]) / 10.0f : i2f(st[2]));
         o[2] = nz ? w.mid / 1e6f : w.mid;
-        o[3] = nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p);
-        o[4] = nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p);
-        o[5] = nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a);
-        o[6] = nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b);
-        o[7] = nz ? i2f(spread) / 1e4f : i2f(spread);
-        o[8] = nz ? i2f(w.step) / 10.0f : i2f(w.step);
+        OBS_I(3, w.best_ask_p, nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p));
+        OBS_I(4, w.best_bid_p, nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p));
+        OBS_I(5, w.vol_a, nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a));
+        OBS_I(6, w.vol_b, nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b));
+        OBS_I(7, spread, nz ? i2f(spread) / 1e4f : i2f(spread));
+        OBS_I(8, w.step, nz ? i2f(w.step) / 10.0f : i2f(w.step));
         o[9] = nz ? trem / (float)c.episode_time : trem;
         return;
     }
-    o[0] = nz ? i2f(st[2]) / 10.0f : i2f(st[2]);
+    // fixed_steps: inventory, mid_price, p_ask, p_bid, q_ask, q_bid, spread, step_counter
+    OBS_I(0, st[2], nz ? i2f(st[2]) / 10.0f : i2f(st[2]));
     o[1] = nz ? w.mid / 1e6f : w.mid;
-    o[2] = nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p);
-    o[3] = nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p);
-    o[4] = nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a);
-    o[5] = nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b);
-    o[6] = nz ? i2f(spread) / 1e4f : i2f(spread);
-    o[7] = nz ? i2f(w.step) / 10.0f : i2f(w.step);
+    OBS_I(2, w.best_ask_p, nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p));
+    OBS_I(3, w.best_bid_p, nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p));
+    OBS_I(4, w.vol_a, nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a));
+    OBS_I(5, w.vol_b, nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b));
+    OBS_I(6, spread, nz ? i2f(spread) / 1e4f : i2f(spread));
+    OBS_I(7, w.step, nz ? i2f(w.step) / 10.0f : i2f(w.step));
 }
-// EXE _get_obs (fixed_steps), sorted keys — exec_env.py:1913-2079
+// EXE _get_obs / _get_obs_basic / _get_obs_simplest_case, sorted keys — exec_env.py:1841-2079
 // ftime: ep_type == fixed_time, passed by the caller (compile-time false in the 100/100 kernel)
+template <bool RAW>
 DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, ObsLane& o,
                  bool ftime) {
-    const bool nz = tc.normalize;
+    const bool nz = !RAW && tc.normalize;
     if (tc.observation_space == HFTLOB_EXE_OBS_BASIC) {  // :1879-1911 best_ask_price, best_bid_price, remaining_quant
         const i32 rq = wsub(st[1], st[2]);
-        o[0] = nz ? i2f(wsub(w.best_ask_p, 1550000)) / 1e3f : i2f(w.best_ask_p);
-        o[1] = nz ? i2f(wsub(w.best_bid_p, 1550000)) / 1e3f : i2f(w.best_bid_p);
-        o[2] = nz ? i2f(rq) / (float)tc.task_size : i2f(rq);
+        OBS_I(0, w.best_ask_p, nz ? i2f(wsub(w.best_ask_p, 1550000)) / 1e3f : i2f(w.best_ask_p));
+        OBS_I(1, w.best_bid_p, nz ? i2f(wsub(w.best_bid_p, 1550000)) / 1e3f : i2f(w.best_bid_p));
+        OBS_I(2, rq, nz ? i2f(rq) / (float)tc.task_size : i2f(rq));
         return;
     }
     if (tc.observation_space == HFTLOB_EXE_OBS_SIMPLEST_CASE) {
-        // :1841-1877 mid_price, percent_remaining_quant, percent_time_remaining
+        // :1841-1877 mid_price, percent_remaining_quant, percent_time_remaining (all float32)
         const float ep = (float)c.episode_time;
         const float ptr = (ep - (i2f(wsub(w.t0, w.it0)) + i2f(wsub(w.t1, w.it1)) / 1e9f)) / ep;
         const float prq = i2f(wsub(st[1], st[2])) / i2f(st[1]);
@@ -1232,65 +1243,48 @@ DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
     const float ip = bitf(st[0]);
     const float ts = (float)tc.task_size;
     const float rr = w.max_steps == 0 ? 0.0f : 1.0f - i2f(w.step) / i2f(w.max_steps);
+    const i32 spr = iabs_(wsub(p_aggr, p_pass)), rq = wsub(st[1], st[2]);
+    int k = 0;
     if (ftime) {
         // fixed_time (exec_env.py:1940-2010): 15 keys, sorted: delta_time, executed_quant, init_price,
         // is_sell_task, p_aggr, p_pass, q_aggr, q_pass, remaining_quant, remaining_ratio, spread,
         // step_counter, task_size, time, time_remaining
-        const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
-        const float te = tm - (i2f(w.it0) + i2f(w.it1) / 1e9f);
-        const float trem = (float)c.episode_time - te;
-        if (nz) {
-            o[0] = w.dt / 10.0f;
-            o[1] = i2f(st[2]) / ts;
-            o[2] = ip / 1e7f;
-            o[3] = i2f(sell) / 1.0f;
-            o[4] = (i2f(p_aggr) - ip) / 1e5f;
-            o[5] = (i2f(p_pass) - ip) / 1e5f;
-            o[6] = i2f(q_aggr) / 1000.0f;
-            o[7] = i2f(q_pass) / 1000.0f;
-            o[8] = i2f(wsub(st[1], st[2])) / ts;
-            o[9] = rr / 1.0f;
-            o[10] = i2f(iabs_(wsub(p_aggr, p_pass))) / 1e4f;
-            o[11] = i2f(w.step) / 30.0f;
-            o[12] = i2f(st[1]) / ts;
-            o[13] = tm / 1e5f;
-            o[14] = trem / (float)c.episode_time;
-        } else {
-            o[0] = w.dt; o[1] = i2f(st[2]); o[2] = ip; o[3] = i2f(sell); o[4] = i2f(p_aggr); o[5] = i2f(p_pass);
-            o[6] = i2f(q_aggr); o[7] = i2f(q_pass); o[8] = i2f(wsub(st[1], st[2])); o[9] = rr;
-            o[10] = i2f(iabs_(wsub(p_aggr, p_pass))); o[11] = i2f(w.step); o[12] = i2f(st[1]); o[13] = tm;
-            o[14] = trem;
-        }
-        return;
+        o[0] = nz ? w.dt / 10.0f : w.dt;
+        k = 1;
     }
-    if (nz) {
-        o[0] = i2f(st[2]) / ts;
-        o[1] = ip / 1e7f;
-        o[2] = i2f(sell) / 1.0f;
-        o[3] = (i2f(p_aggr) - ip) / 1e5f;
-        o[4] = (i2f(p_pass) - ip) / 1e5f;
-        o[5] = i2f(q_aggr) / 1000.0f;
-        o[6] = i2f(q_pass) / 1000.0f;
-        o[7] = i2f(wsub(st[1], st[2])) / ts;
-        o[8] = rr / 1.0f;
-        o[9] = i2f(iabs_(wsub(p_aggr, p_pass))) / 1e4f;
-        o[10] = i2f(w.step) / 30.0f;
-        o[11] = i2f(st[1]) / ts;
-    } else {
-        o[0] = i2f(st[2]); o[1] = ip; o[2] = i2f(sell); o[3] = i2f(p_aggr); o[4] = i2f(p_pass);
-        o[5] = i2f(q_aggr); o[6] = i2f(q_pass); o[7] = i2f(wsub(st[1], st[2])); o[8] = rr;
-        o[9] = i2f(iabs_(wsub(p_aggr, p_pass))); o[10] = i2f(w.step); o[11] = i2f(st[1]);
+    // fixed_steps (12 keys): executed_quant, init_price, is_sell_task, p_aggr, p_pass, q_aggr, q_pass,
+    // remaining_quant, remaining_ratio, spread, step_counter, task_size
+    OBS_I(k + 0, st[2], nz ? i2f(st[2]) / ts : i2f(st[2]));
+    o[k + 1] = nz ? ip / 1e7f : ip;
+    OBS_I(k + 2, sell, nz ? i2f(sell) / 1.0f : i2f(sell));
+    OBS_I(k + 3, p_aggr, nz ? (i2f(p_aggr) - ip) / 1e5f : i2f(p_aggr));
+    OBS_I(k + 4, p_pass, nz ? (i2f(p_pass) - ip) / 1e5f : i2f(p_pass));
+    OBS_I(k + 5, q_aggr, nz ? i2f(q_aggr) / 1000.0f : i2f(q_aggr));
+    OBS_I(k + 6, q_pass, nz ? i2f(q_pass) / 1000.0f : i2f(q_pass));
+    OBS_I(k + 7, rq, nz ? i2f(rq) / ts : i2f(rq));
+    o[k + 8] = nz ? rr / 1.0f : rr;
+    OBS_I(k + 9, spr, nz ? i2f(spr) / 1e4f : i2f(spr));
+    OBS_I(k + 10, w.step, nz ? i2f(w.step) / 30.0f : i2f(w.step));
+    OBS_I(k + 11, st[1], nz ? i2f(st[1]) / ts : i2f(st[1]));
+    if (ftime) {
+        const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
+        const float trem = (float)c.episode_time - (tm - (i2f(w.it0) + i2f(w.it1) / 1e9f));
+        o[13] = nz ? tm / 1e5f : tm;
+        o[14] = nz ? trem / (float)c.episode_time : trem;
     }
 }
-// write one agent's obs row (lanes 0..obs_stride-1 store one float each)
+#undef OBS_I
+// write one agent's obs row (lanes 0..obs_stride-1 store one 32-bit word each);
+// RAW: the un-normalised row of obs_raw
+template <bool RAW>
 DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st,
-                   float* dst, bool zero, bool ftime) {
+                   void* dst, bool zero, bool ftime) {
     const int l = lane_id();
     ObsLane o{l, 0.0f};
-    if (tc.kind == HFTLOB_AGENT_MM) mm_obs(c, tc, w, st, o, ftime);
-    else exe_obs(c, tc, w, st, o, ftime);
+    if (tc.kind == HFTLOB_AGENT_MM) mm_obs<RAW>(c, tc, w, st, o, ftime);
+    else exe_obs<RAW>(c, tc, w, st, o, ftime);
     const float v = zero ? 0.0f : o.v;
-    if (l < c.obs_stride) dst[l] = v;
+    if (l < c.obs_stride) static_cast<float*>(dst)[l] = v;
 }
 
 // ----------------------------------------- reset (MARLEnv.reset_env) device
@@ -1358,7 +1352,7 @@ DEV void env_reset_dev(const hftlob_env_cfg& c, Key key, const i32* __restrict__
             i32 v = 0;
             for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
             if (l < nw) st[l] = v;
-            if (obs) write_obs(c, tc, wv, s, obs + (size_t)ag * c.obs_stride, false, ftime);
+            if (obs) write_obs<false>(c, tc, wv, s, obs + (size_t)ag * c.obs_stride, false, ftime);
             st += nw;
         }
     }
@@ -2157,7 +2151,8 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                       i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
                       const i32* __restrict__ init_states, i32* __restrict__ state, float* __restrict__ obs_out,
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
-                      i32* __restrict__ info_out, i32* lds) {
+                      i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
+                      i32* lds) {
     STAMP(t_start);
     const int l = lane_id();
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
@@ -2352,6 +2347,11 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         } else if (ftime && base > 0) {
             fixed_time_mask(x, y, t_end);
         }
+        if (msgs_out && row < M) {  // the combined message row as the book receives it ("messages" obs)
+            int4* mo = reinterpret_cast<int4*>(msgs_out + ((size_t)e * M + row) * 8);
+            mo[0] = x;
+            mo[1] = y;
+        }
         nx = make_int4(0, 0, 0, 0);
         ny = nx;
         if ((row + 64 >= AR) & (row + 64 < M)) {  // the next chunk's loads land while this one runs
@@ -2484,8 +2484,11 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     i32 v = 0;
                     for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
                     if (l < nw) st[l] = v;
-                    write_obs(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0, ftime);
+                    write_obs<false>(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0, ftime);
                 }
+                if (obs_raw_out)  // the stepped state's raw obs, also on an episode's last step (info)
+                    write_obs<true>(c, tc, wv, s, obs_raw_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, false,
+                                    ftime);
                 st += nw;
             }
         }
@@ -2535,16 +2538,15 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
                                                  const u32* __restrict__ keys, const u32* __restrict__ master,
                                                  u32* __restrict__ master_out, i32* __restrict__ actions_io,
                                                  const i32* __restrict__ msg_data, const i32* __restrict__ init_states,
-                                                 i32* __restrict__ state, float* __restrict__ obs_out,
-                                                 float* __restrict__ rew_out, u8* __restrict__ done_all_out,
-                                                 u8* __restrict__ dones_out, i32* __restrict__ info_out) {
+                                                 i32* __restrict__ state, hftlob_step_out out) {
     extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
     Key mk{0u, 0u};
     if (master) mk = Key{master[0], master[1]};
     env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master != nullptr, mk, actions_io, msg_data, init_states,
-                              state, obs_out, rew_out, done_all_out, dones_out, info_out, lds);
+                              state, out.obs, out.rewards, out.done_all, out.dones, out.info, out.obs_raw, out.msgs,
+                              lds);
     if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
 
@@ -2565,9 +2567,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
                                                     u32* __restrict__ master_out, i32* __restrict__ actions_io,
                                                     const i32* __restrict__ msg_data,
                                                     const i32* __restrict__ init_states, i32* __restrict__ state,
-                                                    float* __restrict__ obs_out, float* __restrict__ rew_out,
-                                                    u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
-                                                    i32* __restrict__ info_out) {
+                                                    hftlob_step_out out) {
     extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
@@ -2585,9 +2585,11 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         const hftlob_env_cfg& cc = *(const hftlob_env_cfg*)cp;
         env_step_dev<S, NFIX, RC>(cc, key_n, key_e0 + e, e, nullptr, true, mk,
                                   actions_io ? actions_io + o * cc.action_words : nullptr, md, is, st,
-                                  obs_out + o * cc.n_agents * cc.obs_stride, rew_out + o * cc.n_agents,
-                                  done_all_out + o, dones_out + o * cc.n_agents,
-                                  info_out ? info_out + o * cc.info_words : nullptr, lds);
+                                  out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents,
+                                  out.done_all + o, out.dones + o * cc.n_agents,
+                                  out.info ? out.info + o * cc.info_words : nullptr,
+                                  out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
+                                  out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr, lds);
     }
     if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
@@ -2710,6 +2712,8 @@ static int check_env(const hftlob_env_cfg* c) {
                 return fail(HFTLOB_EINVAL, "bob_v0 must be positive");
             if (tc.n_action_msgs != 2 || tc.n_msgs != 4) return fail(HFTLOB_EINVAL, "MM message counts");
             if (tc.action_width != 1) return fail(HFTLOB_EINVAL, "MM action_width must be 1");
+            if (tc.observation_space < 0 || tc.observation_space > HFTLOB_MM_OBS_MESSAGES)
+                return fail(HFTLOB_EINVAL, "MM observation_space");
         } else if (tc.kind == HFTLOB_AGENT_EXE) {
             const int a = tc.action_space;
             const int na = a == HFTLOB_EXE_ACT_FIXED_QUANTS_COMPLEX ? 4
@@ -2761,9 +2765,7 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int
     const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
                             12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
 #define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, keys, \
-                                               key_in, key_out, \
-                                               actions, msg_data, init_states, state, out->obs, out->rewards, \
-                                               out->done_all, out->dones, out->info)
+                                               key_in, key_out, actions, msg_data, init_states, state, *out)
     if (cfg->lob.cancel_mode >= 2) {  // random cancel fallback: general sizes only
         if (S == 1) LAUNCH_STEP(1, 0, true);
         else if (S == 2) LAUNCH_STEP(2, 0, true);
@@ -2789,7 +2791,7 @@ static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, 
                             12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
 #define LAUNCH_ROLL(SS, NF, RC) hipLaunchKernelGGL((k_env_rollout<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, \
                                                n_steps, per_step, key_in, key_out, actions, msg_data, init_states, \
-                                               state, out->obs, out->rewards, out->done_all, out->dones, out->info)
+                                               state, *out)
     if (cfg->lob.cancel_mode >= 2) {
         if (S == 1) LAUNCH_ROLL(1, 0, true);
         else if (S == 2) LAUNCH_ROLL(2, 0, true);
@@ -2940,6 +2942,8 @@ int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int key_e0,
             so.done_all = out->done_all + o;
             so.dones = out->dones + o * na;
             so.info = out->info ? out->info + o * cfg->info_words : nullptr;
+            so.obs_raw = out->obs_raw ? out->obs_raw + o * na * cfg->obs_stride : nullptr;
+            so.msgs = out->msgs ? out->msgs + o * (size_t)cfg->n_msgs * 8 : nullptr;
             const uint32_t* kin = t == 0 ? key_in : kb + 2 * ((t - 1) & 1);
             uint32_t* kout = t == n_steps - 1 ? (g == 0 ? key_out : kb + 2 * (t & 1)) : kb + 2 * (t & 1);
             int32_t* acts = actions_out ? actions_out + o * cfg->action_words : nullptr;

@@ -31,7 +31,7 @@ from .data.synthetic import LobsterDay, generate_day
 from .data.windows import Windows, init_messages, loaded_rows, make_windows
 from .engine import book_process_
 from .layout import (AGENT_MM, EXE_FLOAT, action_width, EXE_WORDS, INFO_AGENT_WORDS, INFO_EXE, INFO_MM, INFO_WORLD,
-                     INFO_WORLD_WORDS, MM_FLOAT, MM_WORDS, EnvLayout, StepOut, pack_env_cfg, trader_ids)
+                     INFO_WORLD_WORDS, MM_FLOAT, MM_WORDS, EnvLayout, StepOut, obs_fields, pack_env_cfg, trader_ids)
 
 
 # ------------------------------------------------------------------ spaces
@@ -184,9 +184,19 @@ class MARLEnv:
                               if isinstance(a, Execution_EnvironmentConfig) and a.action_space == "fixed_prices"
                               else Discrete(a.n_actions) for a in self.list_of_agents_configs]
         self.action_words = int(self.cfg_c.action_words)   # int32 words per env of the actions buffer
-        self.observation_spaces = [Box(-1000 if isinstance(a, MarketMaking_EnvironmentConfig) else -10000,
-                                       1000 if isinstance(a, MarketMaking_EnvironmentConfig) else 10000,
-                                       (d,)) for a, d in zip(self.list_of_agents_configs, L.obs_dims)]
+        # MM "messages" (mm_env.py:2820-2821): the observation is the step's combined int32 message
+        # array [M, 8] (the kernel's msgs output), not a float row
+        self.message_obs_types = [isinstance(a, MarketMaking_EnvironmentConfig) and a.observation_space == "messages"
+                                  for a in self.list_of_agents_configs]
+        self.observation_spaces = [
+            Box(-int(w.maxint), int(w.maxint), (a.num_messages_by_agent + w.n_data_msg_per_step, 8), torch.int32)
+            if m else  # mm_env.py:3202-3204 declares num_messages_by_agent + D rows
+            Box(-1000 if isinstance(a, MarketMaking_EnvironmentConfig) else -10000,
+                1000 if isinstance(a, MarketMaking_EnvironmentConfig) else 10000, (d,))
+            for a, d, m in zip(self.list_of_agents_configs, L.obs_dims, self.message_obs_types)]
+        # info["agents"][t]["obs_raw"] (marl_env.py:684-685): (field, dtype) per type, None = messages
+        self.save_raw_observations = bool(w.save_raw_observations)
+        self.obs_raw_fields = [obs_fields(a, w) for a in self.list_of_agents_configs]
         self.return_info = return_info
         self.persistent_outputs = persistent_outputs
         self._out = None
@@ -243,16 +253,26 @@ class MARLEnv:
     def _outputs(self, E: int):
         if self.persistent_outputs and self._out is not None and self._out["obs"].shape[0] == E:
             return self._out
-        L, dev = self.layout, self.device
-        o = {"obs": torch.empty((E, self.num_agents, L.obs_stride), dtype=torch.float32, device=dev),
-             "rewards": torch.empty((E, self.num_agents), dtype=torch.float32, device=dev),
-             "done_all": torch.empty((E,), dtype=torch.bool, device=dev),
-             "dones": torch.empty((E, self.num_agents), dtype=torch.bool, device=dev),
-             "info": torch.empty((E, L.info_words), dtype=torch.int32, device=dev) if self.return_info else None}
-        o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
-                              _lib.ptr(o["dones"]), _lib.ptr(o["info"]) if o["info"] is not None else None)
+        o = self._alloc((E,))
         if self.persistent_outputs:
             self._out = o
+        return o
+
+    def _alloc(self, lead: tuple):
+        """Output buffers of `lead` (E,) or (T, E) env steps and their hftlob_step_out."""
+        L, dev, A = self.layout, self.device, self.num_agents
+        want_raw = self.save_raw_observations and self.return_info
+        o = {"obs": torch.empty(lead + (A, L.obs_stride), dtype=torch.float32, device=dev),
+             "rewards": torch.empty(lead + (A,), dtype=torch.float32, device=dev),
+             "done_all": torch.empty(lead, dtype=torch.bool, device=dev),
+             "dones": torch.empty(lead + (A,), dtype=torch.bool, device=dev),
+             "info": torch.empty(lead + (L.info_words,), dtype=torch.int32, device=dev) if self.return_info else None,
+             "obs_raw": torch.empty(lead + (A, L.obs_stride), dtype=torch.int32, device=dev) if want_raw else None,
+             "msgs": torch.empty(lead + (L.n_msgs, 8), dtype=torch.int32, device=dev)
+             if any(self.message_obs_types) else None}
+        opt = lambda k: _lib.ptr(o[k]) if o[k] is not None else None  # noqa: E731
+        o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
+                              _lib.ptr(o["dones"]), opt("info"), opt("obs_raw"), opt("msgs"))
         return o
 
     def _split_types(self, x: torch.Tensor, obs: bool):
@@ -317,9 +337,31 @@ class MARLEnv:
             d = {}
             for k, (n, isf) in enumerate(fields):
                 d[n] = (f if isf else info).index_select(1, self._info_index(a, n_t, k))
+            if o.get("obs_raw") is not None:
+                d["obs_raw"] = self._obs_raw(o, len(agents), a, n_t, E)
             agents.append(d)
             a += n_t
         return {"world": world, "agents": agents}
+
+    def _obs_raw(self, o, t: int, a: int, n_t: int, E: int):
+        """get_observation(normalize=False, flatten=False) of type t's agents: {field: [E, n_t]}
+        (int32 / float32 as the reference's dict), or the [E, n_t, M, 8] messages."""
+        fields = self.obs_raw_fields[t]
+        if fields is None:
+            return o["msgs"][:, None].expand(E, n_t, self.layout.n_msgs, 8)
+        raw = o["obs_raw"][:, a:a + n_t]
+        rawf = raw.view(torch.float32)
+        return {n: (rawf if dt == "f" else raw)[:, :, k] for k, (n, dt) in enumerate(fields)}
+
+    def _message_obs(self, o, x: torch.Tensor, t: int, a: int, n_t: int, E: int) -> torch.Tensor:
+        """Type t's obs for the MM "messages" space: the combined messages of the step for every
+        agent, zeroed where the agent is done but the env is not (marl_env.py:687-698) and where
+        the env auto-resets (the reset observation is a blank [M, 8] array)."""
+        if not self.message_obs_types[t]:
+            return x
+        m = o["msgs"][:, None].expand(E, n_t, self.layout.n_msgs, 8)
+        zero = o["dones"][:, a:a + n_t] | o["done_all"][:, None]
+        return torch.where(zero[:, :, None, None], torch.zeros((), dtype=m.dtype, device=m.device), m)
 
     def _abi(self, fn: str, *args):
         """Call libhftlob `fn` with this env's device current and torch's current stream OF THAT
@@ -339,7 +381,13 @@ class MARLEnv:
         self._abi("hftlob_env_reset", C.byref(self.cfg_c), E, _lib.ptr(keys),
                   _lib.ptr(params.loaded_params.message_data), _lib.ptr(params.loaded_params.init_states_array),
                   _lib.ptr(buf), C.byref(o["struct"]))
-        return self._split_types(o["obs"], True), self._wrap(buf)
+        obs = self._split_types(o["obs"], True)
+        for t, n_t in enumerate(self.multi_agent_config.number_of_agents_per_type):
+            if self.message_obs_types[t]:
+                # blank messages (mm_env.py:443; the reference's "messages" reset returns None, which its
+                # own auto-reset tree_map cannot select against: a blank array keeps step() defined)
+                obs[t] = torch.zeros((E, n_t, self.layout.n_msgs, 8), dtype=torch.int32, device=self.device)
+        return obs, self._wrap(buf)
 
     reset_env = reset
 
@@ -413,14 +461,7 @@ class MARLEnv:
         if n_slices is None:
             n_slices = self.default_slices(E)
         if per_step:
-            L, dev, T = self.layout, self.device, n_steps
-            o = {"obs": torch.empty((T, E, self.num_agents, L.obs_stride), dtype=torch.float32, device=dev),
-                 "rewards": torch.empty((T, E, self.num_agents), dtype=torch.float32, device=dev),
-                 "done_all": torch.empty((T, E), dtype=torch.bool, device=dev),
-                 "dones": torch.empty((T, E, self.num_agents), dtype=torch.bool, device=dev),
-                 "info": torch.empty((T, E, L.info_words), dtype=torch.int32, device=dev) if self.return_info else None}
-            o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
-                                  _lib.ptr(o["dones"]), _lib.ptr(o["info"]) if o["info"] is not None else None)
+            o = self._alloc((n_steps, E))
             shape = (n_steps, E, self.action_words)
         else:
             o = self._outputs(E)
@@ -446,7 +487,10 @@ class MARLEnv:
 
     def _results(self, o, state, E):
         self.last_info_words = o["info"]  # raw info record of the last step (int32 [E, info_words]) or None
-        obs = self._split_types(o["obs"], True)
+        obs, a = self._split_types(o["obs"], True), 0
+        for t, n_t in enumerate(self.multi_agent_config.number_of_agents_per_type):
+            obs[t] = self._message_obs(o, obs[t], t, a, n_t, E)
+            a += n_t
         rewards = self._split_types(o["rewards"], False)
         dones = {"__all__": o["done_all"], "agents": self._split_types(o["dones"], False)}
         return obs, state, rewards, dones, self._info(o, E)

@@ -70,14 +70,14 @@ class EnvCfg(C.Structure):
 
 class StepOut(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("rewards", C.c_void_p), ("done_all", C.c_void_p),
-                ("dones", C.c_void_p), ("info", C.c_void_p)]
+                ("dones", C.c_void_p), ("info", C.c_void_p), ("obs_raw", C.c_void_p), ("msgs", C.c_void_p)]
 
 
 # ----------------------------------------------------------- enum mappings
 MM_ACTION = {"fixed_quants": 0, "directional_trading": 1, "bobRL": 2, "bobStrategy": 3, "AvSt": 4,
              "spread_skew": 5, "simple": 6}
 AVST_GAMMA = (0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 20.0)       # mm_env.py:1283
-MM_OBS = {"basic": 0, "engineered": 1}
+MM_OBS = {"basic": 0, "engineered": 1, "messages": 2}
 MM_REWARD = {"portfolio_value": 0, "buy_sell_pnl": 1, "complex": 2, "zero_inv": 3, "spooner": 4,
              "spooner_damped": 5, "spooner_asym_damped": 6, "spooner_asym_damped2": 7,
              "spooner_scaled": 8, "delta_portfolio_value": 9}
@@ -120,13 +120,48 @@ EP_TYPE = {"fixed_steps": 0, "fixed_time": 1}
 
 def obs_dim(agent_cfg, world) -> int:
     """observation_space() widths: mm_env.py:3195-3200 (basic 2; engineered 8 fixed_steps, 10 fixed_time);
-    exec_env.py:2185-2200 (engineered: 12 fixed_steps, 15 fixed_time)."""
+    exec_env.py:2185-2200 (engineered: 12 fixed_steps, 15 fixed_time).  The MM "messages" space
+    (mm_env.py:2820-2821) is the step's int32 [M, 8] message array, not a float row: 0 here
+    (its values come from the kernel's msgs output)."""
     if world.ep_type not in EP_TYPE:
         raise ValueError(f"ep_type {world.ep_type!r}: use 'fixed_steps' or 'fixed_time'")
     if isinstance(agent_cfg, MarketMaking_EnvironmentConfig):
-        return {"basic": 2, "engineered": 8 if world.ep_type == "fixed_steps" else 10}[agent_cfg.observation_space]
+        return {"basic": 2, "engineered": 8 if world.ep_type == "fixed_steps" else 10,
+                "messages": 0}[agent_cfg.observation_space]
     return {"engineered": 12 if world.ep_type == "fixed_steps" else 15, "basic": 3,
             "simplest_case": 3}[agent_cfg.observation_space]
+
+
+# get_observation(normalize=False, flatten=False) field names and dtypes ("i" int32, "f" float32), in
+# the sorted-key order of the flattened obs: the save_raw_observations info (marl_env.py:684-685)
+OBS_FIELDS = {
+    ("MM", "basic"): (("inventory", "i"), ("spread", "i")),                     # mm_env.py:2963-3000
+    ("MM", "engineered", "fixed_steps"): (("inventory", "i"), ("mid_price", "f"), ("p_ask", "i"), ("p_bid", "i"),
+                                          ("q_ask", "i"), ("q_bid", "i"), ("spread", "i"), ("step_counter", "i")),
+    ("MM", "engineered", "fixed_time"): (("delta_time", "f"), ("inventory", "i"), ("mid_price", "f"), ("p_ask", "i"),
+                                         ("p_bid", "i"), ("q_ask", "i"), ("q_bid", "i"), ("spread", "i"),
+                                         ("step_counter", "i"), ("time_remaining", "f")),   # mm_env.py:3004-3154
+    ("EXE", "basic"): (("best_ask_price", "i"), ("best_bid_price", "i"), ("remaining_quant", "i")),
+    ("EXE", "simplest_case"): (("mid_price", "f"), ("percent_remaining_quant", "f"), ("percent_time_remaining", "f")),
+    ("EXE", "engineered", "fixed_steps"): (("executed_quant", "i"), ("init_price", "f"), ("is_sell_task", "i"),
+                                           ("p_aggr", "i"), ("p_pass", "i"), ("q_aggr", "i"), ("q_pass", "i"),
+                                           ("remaining_quant", "i"), ("remaining_ratio", "f"), ("spread", "i"),
+                                           ("step_counter", "i"), ("task_size", "i")),
+    ("EXE", "engineered", "fixed_time"): (("delta_time", "f"), ("executed_quant", "i"), ("init_price", "f"),
+                                          ("is_sell_task", "i"), ("p_aggr", "i"), ("p_pass", "i"), ("q_aggr", "i"),
+                                          ("q_pass", "i"), ("remaining_quant", "i"), ("remaining_ratio", "f"),
+                                          ("spread", "i"), ("step_counter", "i"), ("task_size", "i"), ("time", "f"),
+                                          ("time_remaining", "f")),              # exec_env.py:1913-2079
+}
+
+
+def obs_fields(agent_cfg, world):
+    """(name, dtype) of the raw observation dict of one agent type (sorted keys), or None for "messages"."""
+    kind = "MM" if isinstance(agent_cfg, MarketMaking_EnvironmentConfig) else "EXE"
+    space = agent_cfg.observation_space
+    if space == "messages":
+        return None
+    return OBS_FIELDS.get((kind, space)) or OBS_FIELDS[(kind, space, world.ep_type)]
 
 
 @dataclass
@@ -173,7 +208,7 @@ class EnvLayout:
         dims = [obs_dim(t, w) for t in types]
         L = EnvLayout(n_orders=w.nOrders, n_trades=w.nTrades, n_msgs=M, n_data_msg=D, n_action_msgs=A,
                       n_cancel_msgs=M - D - A, agent_kinds=kinds, agent_types=tix, obs_dims=dims,
-                      obs_stride=max(dims))
+                      obs_stride=max(1, max(dims)))
         nO, nT = w.nOrders, w.nTrades
         L.off_asks, L.off_bids, L.off_trades = 0, 6 * nO, 12 * nO
         L.off_loaded = 12 * nO + 8 * nT
@@ -220,7 +255,9 @@ def pack_agent_type(t, n_agents: int, trader_id0: int, world) -> AgentTypeCfg:
         if t.action_space not in MM_ACTION:
             raise ValueError("Invalid action_space specified.")
         if t.observation_space not in MM_OBS:
-            raise NotImplementedError(f"MM observation_space {t.observation_space!r} not implemented")
+            raise NotImplementedError(f"MM observation_space {t.observation_space!r} not implemented (the "
+                                      "'messages_new_tokenizer' space needs the LOB foundation model's tokenizer "
+                                      "config, get_config() of the absent lobgen package, mm_env.py:2824-2960)")
         if t.reward_function not in MM_REWARD:
             raise ValueError("Invalid reward_space specified.")
         if t.inv_penalty not in INV_PEN:

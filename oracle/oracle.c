@@ -1213,6 +1213,7 @@ static void mm_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, Env
         o[1] = nrm(i2f(spread), 1e4f, nz);
         return;
     }
+    if (tc->observation_space == HFTLOB_MM_OBS_MESSAGES) return; /* the obs is the message array (msgs_out) */
     if (c->ep_type == 1) { /* mm_env.py:3029-3088: 10 sorted keys */
         const i32* W = WORLD(E);
         const i32* L = LOADED(E);
@@ -1332,6 +1333,51 @@ static void exe_obs(const hftlob_env_cfg* c, const hftlob_agent_type_cfg* tc, En
     }
 }
 
+/* get_observation(normalize=False, flatten=False) — the dict of save_raw_observations
+ * (marl_env.py:684-685), written in sorted-key order as 32-bit words: int32 fields as
+ * int32, float32 fields as their bits (mm_env.py:2963-3088, exec_env.py:1841-2079).
+ * Restated from the reference dicts, not from the normalised path above. */
+static void agent_obs_raw(const hftlob_env_cfg* c, int t, Env* E, const i32* st, i32* o) {
+    const hftlob_agent_type_cfg* tc = &c->types[t];
+    int M = c->n_msgs, nO = c->lob.n_orders, n = 0;
+    const i32* W = WORLD(E);
+    const i32* L = LOADED(E);
+    i32 pa = BASKS(E)[(M - 1) * 2], pb = BBIDS(E)[(M - 1) * 2];
+    i32 va = side_volume(ASKS(E), nO), vb = side_volume(BIDS(E), nO);
+    float tm = i2f(W[0]) + i2f(W[1]) / 1e9f;
+    float time_remaining = (float)c->episode_time - (tm - (i2f(L[0]) + i2f(L[1]) / 1e9f));
+    for (int k = 0; k < c->obs_stride; ++k) o[k] = 0;
+#define PI(x) (o[n++] = (x))
+#define PF(x) (o[n++] = fbit(x))
+    if (tc->kind == HFTLOB_AGENT_MM) {
+        i32 spread = iabs(wsub(pa, pb));
+        if (tc->observation_space == HFTLOB_MM_OBS_BASIC) { PI(st[2]); PI(spread); return; }  /* inventory, spread */
+        if (tc->observation_space == HFTLOB_MM_OBS_MESSAGES) return;
+        if (c->ep_type == 1) PF(bitf(W[4]));                                   /* delta_time */
+        PI(st[2]); PF(bitf(W[3])); PI(pa); PI(pb); PI(va); PI(vb); PI(spread); PI(L[5]);
+        if (c->ep_type == 1) PF(time_remaining);
+        return;
+    }
+    if (tc->observation_space == HFTLOB_EXE_OBS_BASIC) { PI(pa); PI(pb); PI(wsub(st[1], st[2])); return; }
+    if (tc->observation_space == HFTLOB_EXE_OBS_SIMPLEST_CASE) {
+        i32 tu0 = wsub(W[0], L[0]), tu1 = wsub(W[1], L[1]);
+        float ep = (float)c->episode_time;
+        PF(bitf(W[3]));                                          /* mid_price */
+        PF(i2f(wsub(st[1], st[2])) / i2f(st[1]));                /* percent_remaining_quant */
+        PF((ep - (i2f(tu0) + i2f(tu1) / 1e9f)) / ep);            /* percent_time_remaining */
+        return;
+    }
+    i32 sell = st[3], p_aggr = sell ? pb : pa, p_pass = sell ? pa : pb;
+    i32 ms = L[3], sc = L[5];
+    if (c->ep_type == 1) PF(bitf(W[4]));                         /* delta_time */
+    PI(st[2]); PF(bitf(st[0])); PI(sell); PI(p_aggr); PI(p_pass); PI(sell ? vb : va); PI(sell ? va : vb);
+    PI(wsub(st[1], st[2])); PF(ms == 0 ? 0.0f : 1.0f - i2f(sc) / i2f(ms)); PI(iabs(wsub(p_aggr, p_pass)));
+    PI(sc); PI(st[1]);
+    if (c->ep_type == 1) { PF(tm); PF(time_remaining); }
+#undef PI
+#undef PF
+}
+
 static void agent_obs(const hftlob_env_cfg* c, int t, Env* E, const i32* st, float* o) {
     const hftlob_agent_type_cfg* tc = &c->types[t];
     for (int k = 0; k < c->obs_stride; ++k) o[k] = 0.0f;
@@ -1410,7 +1456,7 @@ int oracle_env_reset(const hftlob_env_cfg* c, int n_env, const u32* keys, const 
 /* ---- MARLEnv.step — marl_env.py:775-804 + step_env :211-709 */
 static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act, const i32* msg_data,
                          const i32* init_states, i32* rec, float* obs, float* rew, i32* done_all, i32* dones,
-                         i32* info) {
+                         i32* info, i32* obs_raw, i32* msgs_out) {
     Env E = {c, rec};
     int part = c->prng_partitionable, M = c->n_msgs, D = c->n_data_msg, A = c->n_action_msgs,
         C = c->n_cancel_msgs, nO = c->lob.n_orders, nT = c->lob.n_trades;
@@ -1484,6 +1530,7 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     }
     memcpy(comb, cnlm, (size_t)C * 8 * sizeof(i32));
     for (int j = 0; j < A; ++j) memcpy(comb + (size_t)(C + j) * 8, actm + (size_t)perm[j] * 8, 8 * sizeof(i32));
+    if (msgs_out) memcpy(msgs_out, comb, (size_t)M * 8 * sizeof(i32)); /* the "messages" observation */
     /* (D) book: trades reinitialised to -1, then the scan */
     i32 asks[HFTLOB_MAX_SLOTS * 6], bids[HFTLOB_MAX_SLOTS * 6], trades[HFTLOB_MAX_SLOTS * 8];
     memcpy(asks, ASKS(&E), (size_t)nO * 6 * sizeof(i32));
@@ -1582,6 +1629,7 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
             dones[a] = d;
             float* o = obs + (size_t)a * c->obs_stride;
             agent_obs(c, t, &E, s, o);
+            if (obs_raw) agent_obs_raw(c, t, &E, s, obs_raw + (size_t)a * c->obs_stride);
             if (d && !all) for (int k = 0; k < c->obs_stride; ++k) o[k] = 0.0f;
         }
     }
@@ -1598,17 +1646,25 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     if (all) env_reset_one(c, key_reset, init_states, rec, obs);
 }
 
-int oracle_env_step(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
-                    const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
-                    i32* info) {
+int oracle_env_step_ex(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
+                       const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
+                       i32* info, i32* obs_raw, i32* msgs) {
     if (!env_cfg_ok(c)) return HFTLOB_EINVAL;
 #pragma omp parallel for schedule(dynamic, 16)
     for (int e = 0; e < n_env; ++e)
         env_step_one(c, keys + 2 * e, actions + (size_t)e * c->action_words, msg_data, init_states,
                      state + (size_t)e * c->rec_words, obs + (size_t)e * c->n_agents * c->obs_stride,
                      rew + (size_t)e * c->n_agents, done_all + e, dones + (size_t)e * c->n_agents,
-                     info ? info + (size_t)e * c->info_words : NULL);
+                     info ? info + (size_t)e * c->info_words : NULL,
+                     obs_raw ? obs_raw + (size_t)e * c->n_agents * c->obs_stride : NULL,
+                     msgs ? msgs + (size_t)e * c->n_msgs * 8 : NULL);
     return HFTLOB_OK;
+}
+int oracle_env_step(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
+                    const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
+                    i32* info) {
+    return oracle_env_step_ex(c, n_env, keys, actions, msg_data, init_states, state, obs, rew, done_all, dones, info,
+                              NULL, NULL);
 }
 
 /* Speed_test.py:166-177 action sampling */
@@ -1734,7 +1790,7 @@ int oracle_rollout_sampled(const hftlob_env_cfg* c, int n_env, int key_e0, int k
             u32 key[2];
             oracle_split(chain + 2 * t, key_n + 1, key_e0 + e + 1, part, key);
             oracle_sample_actions(c, 1, key, acts);
-            env_step_one(c, key, acts, msg_data, init_states, rec, obs, rew, &done_all, dones, NULL);
+            env_step_one(c, key, acts, msg_data, init_states, rec, obs, rew, &done_all, dones, NULL, NULL, NULL);
         }
     }
     master[0] = chain[2 * n_steps];

@@ -27,6 +27,7 @@ def _bind(L):
     L.oracle_book_process.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
     L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.oracle_env_step_ex.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
     L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp]
     L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
@@ -116,8 +117,10 @@ def env_reset(env_cfg, keys, init_states):
     return state, obs
 
 
-def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=True):
-    """Returns (state', obs, rewards, done_all, dones, info); `state` is not modified."""
+def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=True, extras=False):
+    """Returns (state', obs, rewards, done_all, dones, info); `state` is not modified.
+    extras: also return obs_raw (int32 words [E, n_agents, obs_stride], save_raw_observations)
+    and msgs (int32 [E, M, 8], the step's combined messages)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
     E = keys.shape[0]
     actions = np.ascontiguousarray(actions, dtype=np.int32).reshape(E, env_cfg.action_words)
@@ -127,9 +130,14 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
     da = np.zeros(E, dtype=np.int32)
     dn = np.zeros((E, env_cfg.n_agents), dtype=np.int32)
     info = np.zeros((E, env_cfg.info_words), dtype=np.int32) if with_info else None
-    _chk(lib().oracle_env_step(C.byref(env_cfg), E, _p(keys), _p(actions), _p(np.ascontiguousarray(msg_data, np.int32)),
-                               _p(np.ascontiguousarray(init_states, np.int32)), _p(st), _p(obs), _p(rew), _p(da),
-                               _p(dn), _p(info)))
+    raw = np.zeros((E, env_cfg.n_agents, env_cfg.obs_stride), dtype=np.int32) if extras else None
+    msgs = np.zeros((E, env_cfg.n_msgs, 8), dtype=np.int32) if extras else None
+    _chk(lib().oracle_env_step_ex(C.byref(env_cfg), E, _p(keys), _p(actions),
+                                  _p(np.ascontiguousarray(msg_data, np.int32)),
+                                  _p(np.ascontiguousarray(init_states, np.int32)), _p(st), _p(obs), _p(rew), _p(da),
+                                  _p(dn), _p(info), _p(raw), _p(msgs)))
+    if extras:
+        return st, obs, rew, da, dn, info, raw, msgs
     return st, obs, rew, da, dn, info
 
 

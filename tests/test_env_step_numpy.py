@@ -6,7 +6,8 @@ lines and compared with the C oracle on rollouts of the metric config:
   order ids, jax.random.permutation of the action rows and [cancels; actions; data]
   (marl_env.py:254-315); the data window (base_env.py:339-369); the scan
   (oracle/ref_py.py, the numpy engine); abort and _ffill_best_prices (marl_env.py:360-364,
-  723-749); the world update (marl_env.py:488-515).
+  723-749); the world update (marl_env.py:488-515); the combined message array, which is
+  also the MM "messages" observation (mm_env.py:2820-2821).
 
 The agents' action rows come from the numpy restatements of tests/test_mm_actions.py and
 tests/test_exe_variants.py.  Book, trades, best arrays and world words must match bit for bit.
@@ -127,7 +128,7 @@ def numpy_step(cfg, L, prev, key, acts, msg_data):
     mid = f32(f32(int(bb[-1, 0]) + int(ba[-1, 0])) / f32(2))
     dt = f32(f32(f32(f32(f0) + f32(f32(f1) / f32(1e9))) - f32(t0)) - f32(f32(t1) / f32(1e9)))
     return dict(asks=na, bids=nb, trades=ntr, best_asks=ba, best_bids=bb, time=(f0, f1), counter=counter - A,
-                mid=mid, dt=dt, step=int(loaded[5]) + 1, abort=abort)
+                mid=mid, dt=dt, step=int(loaded[5]) + 1, abort=abort, comb=comb)
 
 
 @pytest.mark.parametrize("changes", [dict(), dict(shuffle=False), dict(exe=dict(task="buy")),
@@ -156,7 +157,7 @@ def test_env_step_vs_numpy(changes):
     for k in range(12):
         sk = (keys + 13 * k).astype(np.uint32)
         acts = O.sample_actions(c, sk)
-        post, _, _, done_all, _, info = O.env_step(c, sk, acts, day.msgs, init, st)
+        post, _, _, done_all, _, info, _, msgs = O.env_step(c, sk, acts, day.msgs, init, st, extras=True)
         for e in range(E):
             if done_all[e]:
                 continue
@@ -173,6 +174,8 @@ def test_env_step_vs_numpy(changes):
             assert wr[3:4].view(np.float32)[0] == want["mid"] and wr[4:5].view(np.float32)[0] == want["dt"]
             assert int(p[L.off_loaded + 5]) == want["step"]
             assert bool(info[e, 12]) == want["abort"]
+            # the MM "messages" observation / save_raw_observations messages (mm_env.py:2820-2821)
+            assert np.array_equal(msgs[e], want["comb"]), (k, e, "combined messages")
             checked += 1
         st = post
     assert checked >= 50

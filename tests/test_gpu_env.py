@@ -51,6 +51,24 @@ def _compare_info(env, o, g, tag):
                        equal_nan=True), f"{tag}: info float words differ"
 
 
+def _compare_obs_raw(env, t, a0, n, g, o_raw, o_msgs, tag):
+    """info["agents"][t]["obs_raw"] vs the oracle's raw words: int32 fields bit-exact, float32 fields
+    within RTOL; the messages space: the step's messages, bit-exact."""
+    fields = env.obs_raw_fields[t]
+    if fields is None:
+        assert np.array_equal(g.cpu().numpy(), np.broadcast_to(o_msgs[:, None], g.shape)), f"{tag}: raw messages"
+        return
+    assert list(g) == [f for f, _ in fields]
+    for k, (name, dt) in enumerate(fields):
+        col = o_raw[:, a0:a0 + n, k]
+        got = g[name].cpu().numpy()
+        if dt == "i":
+            assert got.dtype == np.int32 and np.array_equal(got, col), f"{tag}: obs_raw {name}"
+        else:
+            assert got.dtype == np.float32 and np.allclose(got, col.view(np.float32), rtol=RTOL, atol=ATOL), \
+                f"{tag}: obs_raw {name}"
+
+
 def variant(cfg, type_name, **changes):
     """A copy of `cfg` with fields of one agent type replaced (configs are frozen dataclasses)."""
     agents = dict(cfg.dict_of_agents_configs)
@@ -79,9 +97,14 @@ def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True, 
     obs, state = env.reset(keys, params)
     o_state, o_obs = O.env_reset(env.cfg_c, keys.cpu().numpy().view(np.uint32), init)
     _compare_state(env, o_state, state.buf.cpu().numpy(), "reset")
-    assert np.allclose(torch.cat([x.reshape(E, -1) for x in obs], 1).cpu().numpy(),
-                       np.concatenate([o_obs[:, i, :d] for i, d in enumerate(
-                           [env.layout.obs_dims[t] for t in env.layout.agent_types])], 1), rtol=RTOL, atol=1e-6)
+    msg_t = env.message_obs_types
+    for t in range(len(obs)):
+        if msg_t[t]:
+            assert obs[t].dtype == torch.int32 and not obs[t].any(), "messages reset obs is blank"
+    assert np.allclose(torch.cat([x.reshape(E, -1) for t, x in enumerate(obs) if not msg_t[t]], 1).cpu().numpy(),
+                       np.concatenate([o_obs[:, i, :env.layout.obs_dims[t]] for i, t in enumerate(
+                           env.layout.agent_types) if not msg_t[t]], 1), rtol=RTOL, atol=1e-6)
+    extras = env.save_raw_observations or any(msg_t)
     rng = keys
     for k in range(K):
         nk = split_keys(rng, 2, partitionable)
@@ -91,8 +114,8 @@ def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True, 
         assert (acts.cpu().numpy() == o_acts).all(), "device action sampling differs"
         prev = state.buf.cpu().numpy().copy()
         obs, state, rew, dones, info = env.step(sk, state, acts, params)
-        st, oo, orw, oda, odn, oinfo = O.env_step(env.cfg_c, sk.cpu().numpy().view(np.uint32), o_acts, day.msgs,
-                                                  init, prev)
+        res = O.env_step(env.cfg_c, sk.cpu().numpy().view(np.uint32), o_acts, day.msgs, init, prev, extras=extras)
+        st, oo, orw, oda, odn, oinfo = res[:6]
         _compare_state(env, st, state.buf.cpu().numpy(), f"step {k}")
         g_rew = torch.cat([x.reshape(E, -1) for x in rew], 1).cpu().numpy()
         assert np.allclose(g_rew, orw, rtol=RTOL, atol=ATOL), f"step {k}: rewards"
@@ -100,11 +123,79 @@ def rollout_parity(cfg, mid=2_000_000, E=64, K=70, seed=11, partitionable=True, 
         a0 = 0
         for t, n in enumerate(cfg.number_of_agents_per_type):
             d = env.layout.obs_dims[t]
-            assert np.allclose(obs[t].cpu().numpy(), oo[:, a0:a0 + n, :d], rtol=RTOL, atol=1e-6), f"step {k}: obs type {t}"
             g_dn = dones["agents"][t].cpu().numpy()
             assert (g_dn == odn[:, a0:a0 + n].astype(bool)).all(), f"step {k}: dones type {t}"
+            if msg_t[t]:  # the step's messages, blank where the agent is done or the env resets
+                zero = (odn[:, a0:a0 + n].astype(bool) | oda.astype(bool)[:, None])[:, :, None, None]
+                want = np.where(zero, 0, res[7][:, None])
+                assert np.array_equal(obs[t].cpu().numpy(), want), f"step {k}: messages obs type {t}"
+            else:
+                assert np.allclose(obs[t].cpu().numpy(), oo[:, a0:a0 + n, :d], rtol=RTOL, atol=1e-6), \
+                    f"step {k}: obs type {t}"
+            if env.save_raw_observations:
+                _compare_obs_raw(env, t, a0, n, info["agents"][t]["obs_raw"], res[6], res[7], f"step {k}")
             a0 += n
         _compare_info(env, oinfo, env.last_info_words.cpu().numpy(), f"step {k}")
+
+
+def _raw(cfg):
+    return dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, save_raw_observations=True))
+
+
+@pytest.mark.parametrize("mm,exe", [("basic", "engineered"), ("engineered", "basic"), ("engineered", "simplest_case"),
+                                    ("messages", "engineered")])
+def test_save_raw_observations_parity(mm, exe):
+    """info["agents"][t]["obs_raw"] under save_raw_observations (marl_env.py:684-685), the MM
+    "messages" observation (mm_env.py:2820-2821), normalised and not."""
+    cfg = _raw(builtin_config("2_player_fq_fqc"))
+    for norm in (True, False):
+        c = variant(variant(cfg, "MarketMaking", observation_space=mm, normalize=norm), "Execution",
+                    observation_space=exe, normalize=norm)
+        rollout_parity(c, E=32, K=40 if norm else 12)
+
+
+def test_save_raw_observations_fixed_time(tmp_path_factory):
+    day = _loaded("fixed_time", str(tmp_path_factory.mktemp("lob")))
+    cfg = builtin_config("2_player_fq_fqc")
+    w = dataclasses.replace(cfg.world_config, ep_type="fixed_time", episode_time=300, start_resolution=300,
+                            save_raw_observations=True)
+    cfg = variant(dataclasses.replace(cfg, world_config=w), "MarketMaking", observation_space="engineered")
+    rollout_parity(cfg, E=16, K=20, day=day)
+
+
+def test_messages_obs_multi_agent_rollout():
+    """Two MM agents on the messages space, then the sampled rollout (per_step outputs) with
+    save_raw_observations: every step's raw records == an oracle replay from the same keys."""
+    cfg = variant(builtin_config("2_player_fq_fqc"), "MarketMaking", observation_space="messages")
+    cfg = dataclasses.replace(cfg, number_of_agents_per_type=[2, 1])
+    rollout_parity(cfg, E=16, K=20)
+    cfg = _raw(variant(cfg, "Execution", observation_space="basic"))
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
+    params = env.default_params
+    E, T, M = 16, 6, env.layout.n_msgs
+    keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32)).cuda()
+    _, state = env.reset(keys, params)
+    st = state.buf.cpu().numpy()
+    k_in = torch.tensor([0, 7], dtype=torch.int32, device="cuda")
+    k_out = torch.empty_like(k_in)
+    obs, _, _, dones, info = env.rollout_sampled(k_in, k_out, state, params, T, per_step=True, n_slices=1)
+    assert obs[0].shape == (T, E, 2, M, 8) and obs[0].dtype == torch.int32
+    raw_m = info["agents"][0]["obs_raw"].reshape(T, E, 2, M, 8).cpu().numpy()
+    raw_e = {k: v.reshape(T, E, 1).cpu().numpy() for k, v in info["agents"][1]["obs_raw"].items()}
+    assert list(raw_e) == ["best_ask_price", "best_bid_price", "remaining_quant"]
+    init = env._init_states.cpu().numpy()
+    rng = k_in.reshape(1, 2)
+    for k in range(T):
+        ks = split_keys(rng, E + 1, True)[0]
+        rng, sk = ks[0:1].contiguous(), ks[1:].contiguous()
+        sk_np = sk.cpu().numpy().view(np.uint32)
+        acts = O.sample_actions(env.cfg_c, sk_np)
+        st, _, _, oda, odn, _, oraw, omsgs = O.env_step(env.cfg_c, sk_np, acts, env.data.msgs, init, st, extras=True)
+        assert np.array_equal(raw_m[k], np.broadcast_to(omsgs[:, None], (E, 2, M, 8))), f"step {k}: raw msgs"
+        for j, name in enumerate(raw_e):
+            assert np.array_equal(raw_e[name][k], oraw[:, 2:3, j]), f"step {k}: {name}"
+        zero = (odn[:, :2].astype(bool) | oda.astype(bool)[:, None])[:, :, None, None]
+        assert np.array_equal(obs[0][k].cpu().numpy(), np.where(zero, 0, omsgs[:, None])), f"step {k}: obs"
 
 
 @pytest.mark.parametrize("name,mid", [("2_player_fq_fqc", 2_000_000), ("2_player_fq_fqc", 28_000_000),
