@@ -177,11 +177,18 @@ class IPPOTrainer:
         c = config
         for k in ("LR", "GAMMA", "GAE_LAMBDA", "ENT_COEF", "VF_COEF", "MAX_GRAD_NORM", "ANNEAL_LR"):
             c[k] = _per_type(c[k], nt)
-        self.E, self.T = c["NUM_ENVS"], c["NUM_STEPS"]
+        # NUM_ENVS is global, as in the reference's pmap learner: each of the N ranks steps
+        # NUM_ENVS // N envs, NUM_UPDATES = TOTAL_TIMESTEPS // NUM_STEPS // NUM_ENVS
+        # (ippo_rnn_JAXMARL_pmap.py:209-211, 329-332, 419)
+        world = dist.get_world_size() if dist is not None else 1
+        rank = dist.get_rank() if dist is not None else 0
+        n_global = int(c["NUM_ENVS"])
+        if n_global % world:
+            raise ValueError(f"NUM_ENVS ({n_global}) must be a multiple of the world size ({world})")
+        self.E, self.T = n_global // world, c["NUM_STEPS"]
         self.n_agents = list(env.multi_agent_config.number_of_agents_per_type)
         self.n_actors = [n * self.E for n in self.n_agents]
-        world = dist.get_world_size() if dist is not None else 1
-        self.num_updates = max(1, int(c["TOTAL_TIMESTEPS"] // self.T // (self.E * world)))
+        self.num_updates = max(1, int(c["TOTAL_TIMESTEPS"] // self.T // n_global))
         for i, sp in enumerate(env.action_spaces):
             if not isinstance(getattr(sp, "n", None), int):   # the categorical head is Dense(action_space.n)
                 raise NotImplementedError(f"agent type {i}: IPPO-RNN needs a Discrete action space "
@@ -189,7 +196,6 @@ class IPPOTrainer:
         torch.manual_seed(c["SEED"])  # the same initial parameters on every rank
         self.nets = [ActorCriticRNN(env.observation_spaces[i].shape[0], env.action_spaces[i].n, c["FC_DIM_SIZE"],
                                     c["GRU_HIDDEN_DIM"]).to(self.device) for i in range(nt)]
-        world = dist.get_world_size() if dist is not None else 1
         # HIP-graph minibatch steps: single process on the GPU (the grad all-reduce stays eager)
         self.graphs = bool(c.get("CUDA_GRAPHS", False)) and self.device.type == "cuda" and world == 1
         if self.graphs:  # capturable Adam: step counter and lr live on the device
@@ -200,14 +206,16 @@ class IPPOTrainer:
         self._roll = None        # the captured rollout graph (False: not capturable, stays eager)
         self.opt_count = [0] * nt
         self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(c["SEED"] + 1000 * (dist.get_rank() if dist is not None else 0))
+        self.gen.manual_seed(c["SEED"] + 1000 * rank)
         self.params = env.default_params
         self._split = getattr(env, "split_keys", split_keys)   # device threefry split (jax.random.split)
-        rank = dist.get_rank() if dist is not None else 0
-        master = torch.tensor([[c["SEED"], rank]], dtype=torch.int32, device=self.device)
+        # rng = PRNGKey(SEED); rng, _rng = split(rng); reset_rng = split(_rng, NUM_ENVS), sharded over
+        # the ranks in order (:283-284, 329); each rank then draws its step keys from its own rng
+        master = torch.tensor([[0, c["SEED"]]], dtype=torch.int32, device=self.device)
         k = self._split(master, 2)[0]
-        self.rng = k[0].clone()
-        reset_keys = self._split(k[1:2].contiguous(), self.E)[0].contiguous()
+        self.rng = (k[0] if world == 1 else self._split(k[0:1].contiguous(), world)[0][rank]).clone()
+        reset_keys = self._split(k[1:2].contiguous(), n_global)[0][rank * self.E:(rank + 1) * self.E].contiguous()
+        self.reset_keys = reset_keys
         obs, self.state = env.reset(reset_keys, self.params)
         self.last_obs = [o.reshape(n, -1).clone() for o, n in zip(obs, self.n_actors)]
         self.last_done = [torch.zeros(n, dtype=torch.bool, device=self.device) for n in self.n_actors]
@@ -382,7 +390,7 @@ def train(env: MARLEnv, config: Dict, n_updates: Optional[int] = None, dist=None
                  "loss": [{k: float(v) for k, v in d.items()} for d in m["loss"]]})
     sync()
     world = dist.get_world_size() if dist is not None else 1
-    return tr, n * tr.T * tr.E * world / (time.perf_counter() - t0)
+    return tr, n * tr.T * tr.E * world / (time.perf_counter() - t0)   # E * world = NUM_ENVS
 
 
 def main(argv=None) -> None:

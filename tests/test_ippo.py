@@ -164,3 +164,47 @@ def test_grad_pmean_two_ranks():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert pg == [1.5, 1.5, 1.5] and wg == [[5.0, 5.0], [5.0, 5.0]]
+
+
+def _shard_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "jaxmarl-hft_amd"), os.path.join(ROOT, "tests")]
+    import torch.distributed as dist
+    from hftlob.train import ippo as I2
+    from test_ippo import FakeEnv as FE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = I2.default_config(NUM_ENVS=32, NUM_STEPS=4, GRU_HIDDEN_DIM=8, FC_DIM_SIZE=8, NUM_MINIBATCHES=2,
+                          UPDATE_EPOCHS=1, TOTAL_TIMESTEPS=32 * 4 * 10, SEED=3)
+    tr = I2.IPPOTrainer(FE(), c, dist=dist)
+    tr.update()
+    q.put((rank, tr.E, tr.num_updates, tr.reset_keys.tolist(), tr.buf[1].obs.shape[1]))
+    dist.destroy_process_group()
+
+
+def test_num_envs_is_global_over_ranks():
+    """NUM_ENVS is the global env count (ippo_rnn_JAXMARL_pmap.py:209-211, 329): 2 ranks step 16
+    envs each, NUM_UPDATES = TOTAL // NUM_STEPS // NUM_ENVS, and the ranks' reset keys are the
+    two halves of one split(_rng, NUM_ENVS)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(i, 2, port, q)) for i in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    env = FakeEnv()
+    c = I.default_config(NUM_ENVS=32, NUM_STEPS=4, GRU_HIDDEN_DIM=8, FC_DIM_SIZE=8, NUM_MINIBATCHES=2,
+                         UPDATE_EPOCHS=1, TOTAL_TIMESTEPS=32 * 4 * 10, SEED=3)
+    single = I.IPPOTrainer(env, c)                     # 1 rank: all 32 envs, the same global keys
+    assert single.E == 32 and single.num_updates == 10
+    for rank, E, nu, keys, actors in res:
+        assert (E, nu, actors) == (16, 10, 32)        # type 1 has 2 agents per env
+        assert keys == single.reset_keys[16 * rank:16 * (rank + 1)].tolist()
+    with pytest.raises(ValueError, match="multiple of the world size"):
+        class _D:
+            get_world_size = staticmethod(lambda: 3)
+            get_rank = staticmethod(lambda: 0)
+        I.IPPOTrainer(env, c, dist=_D())
