@@ -65,3 +65,66 @@ def test_graph_rollout_replays_the_env_exactly():
             if t + 1 < T:
                 assert torch.equal(obs[i].reshape(obs_next[i].shape[1], -1), obs_next[i][t + 1]), (t, i)
     assert torch.equal(state.buf, tr.state.buf)
+
+
+def test_learner_on_device_matches_numpy():
+    """A recorded device rollout through the GPU learner: GAE and the PPO loss terms against the
+    float64 numpy restatements of tests/test_ippo.py (ippo_rnn_JAXMARL.py:668-765) at rtol 1e-5,
+    and one minibatch step (gradient, global-norm clip, Adam) against a float64 CPU copy of the
+    network with the clip (optax clip_by_global_norm) and Adam (optax.adam, eps 1e-5) in numpy."""
+    import copy
+    from test_ippo import np_gae, np_ppo_loss
+    cfg = builtin_config("2_player_fq_fqc")
+    w = cfg.world_config
+    day = generate_day(n_msgs=30_000, seed=4, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    env = MARLEnv(None, cfg, data=day, return_info=False, persistent_outputs=True)
+    E, T, MB = 64, 12, 2
+    c = I.default_config(NUM_ENVS=E, NUM_STEPS=T, GRU_HIDDEN_DIM=32, FC_DIM_SIZE=32, NUM_MINIBATCHES=MB,
+                         UPDATE_EPOCHS=1, TOTAL_TIMESTEPS=E * T * 4, GAMMA=[0.99, 0.95], GAE_LAMBDA=[0.9, 0.95])
+    tr = I.IPPOTrainer(env, c)
+    for _ in range(3):                     # some episodes progress; rewards become non-trivial
+        tr.update()
+    h0 = [h.clone() for h in tr.h]
+    tr.rollout()
+    npy = lambda x: x.detach().double().cpu().numpy()  # noqa: E731
+    for i, net in enumerate(tr.nets):
+        b, n = tr.buf[i], tr.n_actors[i]
+        with torch.no_grad():
+            _, _, last_val = net.step(tr.h[i], tr.last_obs[i], tr.last_done[i])
+            adv, tgt = I.calculate_gae(b.reward, b.value, b.global_done, last_val, c["GAMMA"][i], c["GAE_LAMBDA"][i])
+        want_adv, want_tgt = np_gae(npy(b.reward), npy(b.value), npy(b.global_done), npy(last_val),
+                                    c["GAMMA"][i], c["GAE_LAMBDA"][i])
+        assert np.allclose(npy(adv), want_adv, rtol=1e-5, atol=1e-5), f"type {i}: GAE"
+        assert np.allclose(npy(tgt), want_tgt, rtol=1e-5, atol=1e-5), f"type {i}: targets"
+        idx = torch.randperm(n, device=tr.device, generator=torch.Generator(device=tr.device).manual_seed(i))[:n // MB]
+        eps, vf, ent = c["CLIP_EPS"], c["VF_COEF"][i], c["ENT_COEF"][i]
+        with torch.no_grad():
+            logits, values = net(h0[i][idx], b.obs[:, idx], b.done[:, idx])
+            out = I.ppo_loss(logits, values, b.action[:, idx], b.value[:, idx], b.log_prob[:, idx], adv[:, idx],
+                             tgt[:, idx], eps, vf, ent)
+        want = np_ppo_loss(npy(logits), npy(values), npy(b.action[:, idx]).astype(np.int64), npy(b.value[:, idx]),
+                           npy(b.log_prob[:, idx]), npy(adv[:, idx]), npy(tgt[:, idx]), eps, vf, ent)
+        assert np.allclose([float(x) for x in out[:4]], want, rtol=1e-5, atol=1e-6), f"type {i}: loss terms"
+        # one minibatch step through the trainer (fresh Adam state) vs float64 on the CPU
+        ref = copy.deepcopy(net).double().cpu()
+        tr.opts[i] = torch.optim.Adam(net.parameters(), lr=c["LR"][i], eps=1e-5)
+        st = tr._static(i, n, MB)
+        st["h0"].copy_(h0[i]); st["adv"].copy_(adv); st["tgt"].copy_(tgt); st["idx"].copy_(idx)
+        tr.opts[i].zero_grad(set_to_none=True)
+        tr._mb_step(i)
+        cpu = lambda x: x.detach().cpu()  # noqa: E731
+        lg, vv = ref(cpu(h0[i][idx]).double(), cpu(b.obs[:, idx]).double(), cpu(b.done[:, idx]))
+        loss = I.ppo_loss(lg, vv, cpu(b.action[:, idx]), cpu(b.value[:, idx]).double(), cpu(b.log_prob[:, idx]).double(),
+                          cpu(adv[:, idx]).double(), cpu(tgt[:, idx]).double(), eps, vf, ent)[0]
+        loss.backward()
+        grads = [p.grad.numpy() for p in ref.parameters()]
+        norm = np.sqrt(sum((g ** 2).sum() for g in grads))
+        mx = c["MAX_GRAD_NORM"][i]
+        scale = 1.0 if norm < mx else mx / norm
+        lr = c["LR"][i]
+        for (name, p_dev), p_ref, g in zip(net.named_parameters(), ref.parameters(), grads):
+            g = g * scale
+            m, v = 0.1 * g, 0.001 * g * g                         # first Adam step, b1 0.9, b2 0.999
+            upd = lr * (m / 0.1) / (np.sqrt(v / 0.001) + 1e-5)
+            want_p = p_ref.detach().numpy() - upd
+            assert np.allclose(npy(p_dev), want_p, rtol=1e-5, atol=lr * 2e-3), f"type {i}: {name} after one step"

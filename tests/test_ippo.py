@@ -16,6 +16,35 @@ from hftlob.train import ippo as I
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def np_gae(r, v, d, last, gamma, lam):
+    """_calculate_gae / _get_advantages (:668-690) in float64: (advantages, targets)."""
+    T, B = r.shape
+    adv = np.zeros((T, B), np.float64)
+    gae, nv = np.zeros(B), np.asarray(last, np.float64)
+    for t in reversed(range(T)):          # reverse scan carrying (gae, next_value)
+        delta = r[t] + gamma * nv * (1 - d[t]) - v[t]
+        gae = delta + gamma * lam * (1 - d[t]) * gae
+        adv[t] = gae
+        nv = v[t].astype(np.float64)
+    return adv, adv + v
+
+
+def np_ppo_loss(logits, values, act, old_v, old_lp, gae, targets, eps, vf, ent):
+    """_loss_fn (:718-765) in float64: (total, value_loss, actor_loss, entropy)."""
+    logits, values, old_v, old_lp, gae, targets = (np.asarray(x, np.float64) for x in
+                                                   (logits, values, old_v, old_lp, gae, targets))
+    lp_all = logits - logits.max(-1, keepdims=True)
+    lp_all = lp_all - np.log(np.exp(lp_all).sum(-1, keepdims=True))
+    lp = np.take_along_axis(lp_all, np.asarray(act)[..., None], -1)[..., 0]
+    vpc = old_v + np.clip(values - old_v, -eps, eps)
+    vloss = 0.5 * np.maximum((values - targets) ** 2, (vpc - targets) ** 2).mean()
+    ratio = np.exp(lp - old_lp)
+    g = (gae - gae.mean()) / (gae.std() + 1e-8)
+    aloss = -np.minimum(ratio * g, np.clip(ratio, 1 - eps, 1 + eps) * g).mean()
+    entropy = -(np.exp(lp_all) * lp_all).sum(-1).mean()
+    return aloss + vf * vloss - ent * entropy, vloss, aloss, entropy
+
+
 def test_gae_matches_reference_formula():
     rng = np.random.default_rng(0)
     T, B = 9, 5
@@ -23,13 +52,7 @@ def test_gae_matches_reference_formula():
     d = rng.random((T, B)) < 0.2
     last = rng.normal(size=B).astype(np.float32)
     gamma, lam = 0.99, 0.9
-    adv = np.zeros((T, B), np.float64)
-    gae, nv = np.zeros(B), last.astype(np.float64)
-    for t in reversed(range(T)):          # _get_advantages: reverse scan carrying (gae, next_value)
-        delta = r[t] + gamma * nv * (1 - d[t]) - v[t]
-        gae = delta + gamma * lam * (1 - d[t]) * gae
-        adv[t] = gae
-        nv = v[t]
+    adv, _ = np_gae(r, v, d, last, gamma, lam)
     a, tg = I.calculate_gae(torch.from_numpy(r), torch.from_numpy(v), torch.from_numpy(d), torch.from_numpy(last),
                             gamma, lam)
     assert np.allclose(a.numpy(), adv, atol=1e-5) and np.allclose(tg.numpy(), adv + v, atol=1e-5)
@@ -44,15 +67,7 @@ def test_ppo_loss_matches_reference_formula():
     old_v, old_lp = rng.normal(size=(T, B)).astype(np.float32), -rng.random((T, B)).astype(np.float32)
     gae, targets = rng.normal(size=(T, B)).astype(np.float32), rng.normal(size=(T, B)).astype(np.float32)
     eps, vf, ent = 0.2, 0.5, 0.01
-    lp_all = logits - np.log(np.exp(logits).sum(-1, keepdims=True))
-    lp = np.take_along_axis(lp_all, act[..., None], -1)[..., 0]
-    vpc = old_v + np.clip(values - old_v, -eps, eps)
-    vloss = 0.5 * np.maximum((values - targets) ** 2, (vpc - targets) ** 2).mean()
-    ratio = np.exp(lp - old_lp)
-    g = (gae - gae.mean()) / (gae.std() + 1e-8)
-    aloss = -np.minimum(ratio * g, np.clip(ratio, 1 - eps, 1 + eps) * g).mean()
-    entropy = -(np.exp(lp_all) * lp_all).sum(-1).mean()
-    total = aloss + vf * vloss - ent * entropy
+    total, vloss, aloss, entropy = np_ppo_loss(logits, values, act, old_v, old_lp, gae, targets, eps, vf, ent)
     out = I.ppo_loss(*(torch.from_numpy(x) for x in (logits, values, act, old_v, old_lp, gae, targets)), eps, vf, ent)
     assert np.allclose([float(x) for x in out[:4]], [total, vloss, aloss, entropy], rtol=1e-5, atol=1e-6)
 
