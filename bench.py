@@ -331,7 +331,8 @@ def main(argv=None):
                      "salu_per_env_step": prof["salu_per_env_step"], "source": prof.get("source")}
     workload = (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, {env.num_msgs_per_step} msgs/step, "
                 "auto-reset, Speed_test semantics" if metric_cfg else
-                f"{args.config}.json agents {list(cfg.number_of_agents_per_type)}, {env.num_msgs_per_step} msgs/step, "
+                f"{args.config if args.config == 'default' else args.config + '.json'} "
+                f"agents {list(cfg.number_of_agents_per_type)}, {env.num_msgs_per_step} msgs/step, "
                 "auto-reset, Speed_test semantics")
     line = {
         "metric": "env steps/sec (whole node), 2-agent MARL, 10-level LOB, NUM_ENVS=4096",

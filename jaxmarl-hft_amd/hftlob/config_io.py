@@ -77,5 +77,10 @@ CONFIG_DIR = os.path.join(os.path.dirname(__file__), "configs")
 
 
 def builtin_config(name: str) -> MultiAgentConfig:
-    """Load one of the env configs shipped under ``hftlob/configs`` by file stem."""
+    """Load one of the env configs shipped under ``hftlob/configs`` by file stem; ``"default"`` is
+    ``MultiAgentConfig()`` itself (MM bobRL / engineered + EXE fixed_quants_complex, world defaults):
+    the config Speed_test.py:101-113 times (its list_of_agents_configs attribute is not read by
+    MARLEnv, which iterates dict_of_agents_configs, marl_env.py:71)."""
+    if name == "default":
+        return MultiAgentConfig()
     return load_config_from_file(os.path.join(CONFIG_DIR, name + ".json"))

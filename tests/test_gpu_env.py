@@ -506,3 +506,38 @@ def test_max_book_size_parity():
     cfg = builtin_config("2_player_fq_fqc")
     cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, nOrders=256, nTrades=256))
     rollout_parity(cfg, E=16, K=40)
+
+
+SWEEP = [(ag, D) for ag in ([1, 1], [5, 5], [10, 10]) for D in (100, 1)]
+
+
+def speed_test_config(agents, D, episode_time=32):
+    """Speed_test.py:50-71, 101-113: MultiAgentConfig() (MM bobRL + EXE fixed_quants_complex) with
+    agents per type and n_data_msg_per_step D; the parity runs use 32-step episodes (the bench
+    rows keep the default 6400) so a short rollout crosses the auto-reset."""
+    cfg = builtin_config("default")
+    w = dataclasses.replace(cfg.world_config, n_data_msg_per_step=D, episode_time=episode_time,
+                            start_resolution=episode_time)
+    return dataclasses.replace(cfg, world_config=w, number_of_agents_per_type=list(agents))
+
+
+@pytest.mark.parametrize("agents,D", SWEEP, ids=lambda x: str(x))
+def test_speed_test_sweep_parity(agents, D):
+    """Speed_test's sweep ([1,1] / [5,5] / [10,10] agents x 100 / 1 data messages; [10,10] is 120
+    agent message rows): env.step vs the oracle over an auto-reset, then the sampled rollout
+    (the bench path, 2 slices) vs the oracle's C rollout loop: state and carried key."""
+    cfg = speed_test_config(agents, D)
+    rollout_parity(cfg, E=16, K=40)
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
+    params = env.default_params
+    E, T = 24, 40
+    keys = torch.from_numpy(np.arange(2 * E, dtype=np.uint32).reshape(E, 2).view(np.int32) + 5).cuda()
+    _, state = env.reset(keys, params)
+    s0 = state.buf.cpu().numpy()
+    k_in = torch.tensor([0, 42], dtype=torch.int32, device="cuda")
+    k_out = torch.empty_like(k_in)
+    env.rollout_sampled(k_in, k_out, state, params, T, n_slices=2)
+    o_st, o_key = O.rollout_sampled(env.cfg_c, k_in.cpu().numpy().view(np.uint32), env.data.msgs,
+                                    env._init_states.cpu().numpy(), s0, T)
+    _compare_state(env, o_st, state.buf.cpu().numpy(), "rollout_sampled")
+    assert (k_out.cpu().numpy().view(np.uint32) == o_key).all(), "carried key"

@@ -7,6 +7,7 @@ T=${1:-r01}
 O=$GRAFT_REPO_ROOT/gpurun_out/prof_$T
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
+[ -n "$SKIP_TESTS" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || exit 8
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 9
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 cd /tmp && export TMPDIR=/tmp

@@ -1,6 +1,8 @@
 """Summarise a tools/profile_round.sh directory: kernel stats, HBM traffic per
 k_env_step launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), SQ counters
-per wave.  Writes <dir>/pmc_traffic.json and prints a text summary."""
+per wave.  Writes <dir>/pmc_traffic.json and <dir>/kernel_profile.json (what bench.py
+reads from profiles/rNN_kernel_profile.json for the roofline's traffic and the issue
+roofline) and prints a text summary."""
 import csv
 import glob
 import json
@@ -21,15 +23,20 @@ def per_launch(sub, counter, kernel="k_env_step"):
 
 
 stats = glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursive=True)
+kstat = None
 if stats:
     print("== rocprofv3 --kernel-trace --stats (bench.py --no-cpu-baseline)")
     for r in csv.DictReader(open(stats[0])):
         print(f"{r['Name'][:60]:60s} calls {r['Calls']:>6s} avg_ns {float(r['AverageNs']):12.1f} "
               f"total_pct {float(r['Percentage']):6.2f}")
+        if "k_env_step" in r["Name"] and kstat is None:
+            kstat = {"kernel_avg_us": round(float(r["AverageNs"]) / 1e3, 2), "launches": int(r["Calls"]),
+                     "kernel_name": r["Name"]}
 fetch_kb, write_kb = per_launch("fetch", "FETCH_SIZE"), per_launch("write", "WRITE_SIZE")
 bench = json.load(open(os.path.join(d, "stats_bench.json"))) if os.path.exists(os.path.join(d, "stats_bench.json")) else {}
 E = bench.get("config", {}).get("num_envs_per_gpu", 4096)
-G = bench.get("roofline", {}).get("slices", 1)  # env slices: one k_env_step launch steps E / G envs
+G = bench.get("roofline", {}).get("launches_per_step", bench.get("roofline", {}).get("slices", 1))
+# env slices: one k_env_step launch steps E / G envs
 out = {}
 if fetch_kb is not None and write_kb is not None:
     hbm = (2 * fetch_kb + write_kb) * 1024
@@ -43,10 +50,11 @@ sq = {}
 for r in rows("sq"):
     if "k_env_step" in r["Kernel_Name"]:
         sq.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+per_wave = {}
 if sq:
     w = sum(sq["SQ_WAVES"]) / len(sq["SQ_WAVES"])
-    print("== SQ counters per wave (k_env_step):",
-          {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(sq.items()) if k != "SQ_WAVES"})
+    per_wave = {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(sq.items()) if k != "SQ_WAVES"}
+    print("== SQ counters per wave (k_env_step):", per_wave)
 lds = {}
 for r in rows("lds"):
     if "k_env_step" in r["Kernel_Name"]:
@@ -60,3 +68,15 @@ if os.path.exists(sm) and os.path.getsize(sm):
     b = json.load(open(sm))
     print("== step mode (split_keys + sample_actions + env.step, 3 launches):", b["value"], "env steps/s,",
           b["ms_per_step"], "ms/step")
+
+# one wave per env and one env-step per wave per k_env_step launch: per-wave counts are per env-step
+prof = dict(kstat or {})
+prof.update({"envs_per_launch": E // G, "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d))})
+if "INSTS_SALU" in per_wave:
+    prof["salu_per_env_step"] = per_wave["INSTS_SALU"]
+    prof["valu_per_env_step"] = per_wave.get("INSTS_VALU")
+    prof["wave_cycles_per_env_step"] = per_wave.get("WAVE_CYCLES")
+if out:
+    prof["hbm_bytes_per_env_step"] = out["hbm_bytes_per_env_step"]
+json.dump(prof, open(os.path.join(d, "kernel_profile.json"), "w"), indent=1)
+print("== kernel_profile.json:", json.dumps(prof))
