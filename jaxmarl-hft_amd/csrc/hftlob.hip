@@ -127,6 +127,12 @@ DEV i32 sel(bool c, i32 a, i32 b) {
     asm volatile("" : "+v"(b));
     return c ? a : b;
 }
+// pin a per-lane value in its VGPR: a chain of selects on it stays a chain of VALU selects
+// (v_cmp + v_cndmask) instead of being folded into 64-bit lane-mask logic on the scalar unit
+DEV u32 vkeep(u32 v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 DEV float self(bool c, float a, float b) {  // (uniform floats live in VGPRs: the VALU computes them)
     asm volatile("" : "+v"(a));
     asm volatile("" : "+v"(b));
@@ -591,7 +597,7 @@ struct Book {
 
 // message handler codes (the reference's dispatch index) and flags, see decode_msgs
 enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8, H_NEG1 = 16,
-       H_PM1 = 32 };
+       H_PM1 = 32, H_MKT = 64 };
 struct Msg {
     i32 h, side, price, qty, oid, tid, t, tns;  // h: handler code and H_* flags (decode_msgs)
 };
@@ -709,6 +715,15 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
 // a crossing trip loads every column it needs at once (one LDS round trip)
 template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     const int R = B.c.nO;
+    // the common case first, as straight-line scalar code: nothing to match, or a best that
+    // does not cross (the loop's own first test, with an empty ask side standing for maxint)
+    if (qtm <= 0) return qtm;
+    if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+    {
+        const i32 bp = s.best_p;
+        const i32 mp0 = (!BID && bp == -1) ? B.c.maxint : bp;
+        if (__builtin_expect(BID ? mp0 < price : mp0 > price, 1)) return qtm;
+    }
     while (qtm > 0) {
         if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
         // the side's best; an empty ask side (-1) counts as maxint (_get_top_ask_order_idx).
@@ -824,6 +839,8 @@ template <bool BID, int S> DEV void add_free(Book<S>& B, Side<S>& s, const Msg& 
     for (int r = 1; r < S; ++r) e = min(e, ff1(free[r]) | (u32)(64 * r));
     side_put(s, R, (int)e, m.price, qty, m.oid, m.tid, m.t, m.tns);
     if (__builtin_expect((m.h & (H_NEG1 | H_PM1)) != 0, 0)) {
+        // rare: kept as a branch (the empty asm stops if-conversion into ~10 scalar selects per add)
+        asm volatile("");
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
     }
@@ -832,14 +849,13 @@ template <bool BID, int S> DEV void add_free(Book<S>& B, Side<S>& s, const Msg& 
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
-    if (__builtin_expect(B.c.t4 == 2, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
+    if (__builtin_expect((m.h & H_MKT) != 0, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
     lmask free[S];
     free_slots(B, B.b, free);
     if (!no_slot(free)) {
-        if (!(m.h & H_DISCARD)) {
-            if (!G) add_free<true>(B, B.b, m, rem, free);
-            else add_order<true, G>(B, B.b, m, rem, free);
-        }
+        // FAST: a discarded add is an add of nothing (add_free returns at once for qty <= 0)
+        if (!G) add_free<true>(B, B.b, m, (m.h & H_DISCARD) ? 0 : rem, free);
+        else if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
         return;
     }
     if (B.c.check_fill) evict_if_full<true>(B, B.b, free);
@@ -847,15 +863,13 @@ template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
 }
 // ask_lim — :446-508
 template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
-    if (__builtin_expect(B.c.t4 == 2, 0)) m.price = 0;
+    if (__builtin_expect((m.h & H_MKT) != 0, 0)) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
     lmask free[S];
     free_slots(B, B.a, free);
     if (!no_slot(free)) {
-        if (!(m.h & H_DISCARD)) {
-            if (!G) add_free<false>(B, B.a, m, rem, free);
-            else add_order<false, G>(B, B.a, m, rem, free);
-        }
+        if (!G) add_free<false>(B, B.a, m, (m.h & H_DISCARD) ? 0 : rem, free);
+        else if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, free);
         return;
     }
     if (B.c.check_fill) evict_if_full<false>(B, B.a, free);
@@ -923,9 +937,9 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
         const u32 span = (u32)wsub(B.c.init_id, lo);
 #pragma unroll
         for (int r = 0; r < S; ++r) {
-            u32 d = (u32)wsub(o[r], lo);
-            d = s.pc[r] == m.price ? d : 0xFFFFFFFFu;
-            d = q[r] >= m.qty ? d : 0xFFFFFFFFu;
+            u32 d = vkeep((u32)wsub(o[r], lo));
+            d = vkeep(s.pc[r] == m.price ? d : 0xFFFFFFFFu);
+            d = vkeep(q[r] >= m.qty ? d : 0xFFFFFFFFu);
             fm[r] = B.vs.m[r] & bal(d <= span);
         }
         if (!RC) {
@@ -980,6 +994,7 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     const i32 p_add = c.t4 == 2 ? (h == H_BID ? c.maxint : 0) : x.w;
     if ((p_add != -1) & ((y.x == -1) | (y.y == -1) | (y.z == -1) | (y.w == -1))) h |= H_NEG1;
     if (p_add == -1) h |= H_PM1;  // an add would write an order priced -1
+    if (c.t4 == 2) h |= H_MKT;    // type_4_interpretation MKT: the limit handlers' price overrides
     x.x = h;
     x.y = sd;
 }
