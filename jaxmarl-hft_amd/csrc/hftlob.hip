@@ -354,9 +354,10 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 //          row holds a -1 <=> its price is -1 <=> it is all -1, so the free slots are the
 //          p == -1 slots of the register price column
 // (bit 0 is left unused: a branch on a bit-0 test compiles to s_bitcmp1 + a 64-bit lane mask
-// + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc)
-enum : u32 { F_OK_A = 2, F_OK_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64, F_FAST = 128,
-             F_PM1_A = 256, F_PM1_B = 512 };
+// + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc.  F_FAST,
+// tested once per message, is the sign bit: (i32)fl < 0 is one s_cmp_lt_i32)
+enum : u32 { F_OK_A = 2, F_OK_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64,
+             F_PM1_A = 256, F_PM1_B = 512, F_FAST = 0x80000000u };
 template <bool ASKS> struct SideBits {
     static constexpr u32 OK = ASKS ? F_OK_A : F_OK_B;
     static constexpr u32 CLEAN = ASKS ? F_CLEAN_A : F_CLEAN_B;
@@ -597,7 +598,7 @@ struct Book {
 
 // message handler codes (the reference's dispatch index) and flags, see decode_msgs
 enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7, H_DISCARD = 8, H_NEG1 = 16,
-       H_PM1 = 32, H_MKT = 64 };
+       H_PM1 = 32, H_MKT = 64, H_RARE = 128 };
 struct Msg {
     i32 h, side, price, qty, oid, tid, t, tns;  // h: handler code and H_* flags (decode_msgs)
 };
@@ -717,7 +718,8 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
     const int R = B.c.nO;
     // the common case first, as straight-line scalar code: nothing to match, or a best that
     // does not cross (the loop's own first test, with an empty ask side standing for maxint)
-    if (qtm <= 0) return qtm;
+    // (fresh: the RARE / common handler copies each keep their own test, not one shared lane mask)
+    if (fresh(qtm) <= 0) return qtm;
     if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
     {
         const i32 bp = s.best_p;
@@ -831,14 +833,15 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
 // The common add: FAST book, a free (all -1) slot exists, no eviction: the order goes to the
 // first free slot (add_order's "first row holding any -1").  Flag changes are rare (orders with
 // -1 fields), so they stay behind a branch.
-template <bool BID, int S> DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
+template <bool BID, bool RARE, int S>
+DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
     if (qty <= 0) return;  // imax(0, qty) == 0: the new row is removed at once and the slot was empty
     u32 e = ff1(free[0]);
 #pragma unroll
     for (int r = 1; r < S; ++r) e = min(e, ff1(free[r]) | (u32)(64 * r));
     side_put(s, R, (int)e, m.price, qty, m.oid, m.tid, m.t, m.tns);
-    if (__builtin_expect((m.h & (H_NEG1 | H_PM1)) != 0, 0)) {
+    if (RARE && __builtin_expect((m.h & (H_NEG1 | H_PM1)) != 0, 0)) {
         // rare: kept as a branch (the empty asm stops if-conversion into ~10 scalar selects per add)
         asm volatile("");
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
@@ -847,14 +850,16 @@ template <bool BID, int S> DEV void add_free(Book<S>& B, Side<S>& s, const Msg& 
     note_add<BID>(s, B.fl, m.price, qty, B.c.maxint);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
-template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
+// RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
+// tests are compiled out of the common FAST add
+template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
-    if (__builtin_expect((m.h & H_MKT) != 0, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
+    if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
     lmask free[S];
     free_slots(B, B.b, free);
     if (!no_slot(free)) {
         // FAST: a discarded add is an add of nothing (add_free returns at once for qty <= 0)
-        if (!G) add_free<true>(B, B.b, m, (m.h & H_DISCARD) ? 0 : rem, free);
+        if (!G) add_free<true, RARE>(B, B.b, m, (RARE && (m.h & H_DISCARD)) ? 0 : rem, free);
         else if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
         return;
     }
@@ -862,13 +867,13 @@ template <bool G, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
 }
 // ask_lim — :446-508
-template <bool G, int S> DEV void ask_lim(Book<S>& B, Msg m) {
-    if (__builtin_expect((m.h & H_MKT) != 0, 0)) m.price = 0;
+template <bool G, bool RARE, int S> DEV void ask_lim(Book<S>& B, Msg m) {
+    if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
     lmask free[S];
     free_slots(B, B.a, free);
     if (!no_slot(free)) {
-        if (!G) add_free<false>(B, B.a, m, (m.h & H_DISCARD) ? 0 : rem, free);
+        if (!G) add_free<false, RARE>(B, B.a, m, (RARE && (m.h & H_DISCARD)) ? 0 : rem, free);
         else if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, free);
         return;
     }
@@ -995,6 +1000,7 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     if ((p_add != -1) & ((y.x == -1) | (y.y == -1) | (y.z == -1) | (y.w == -1))) h |= H_NEG1;
     if (p_add == -1) h |= H_PM1;  // an add would write an order priced -1
     if (c.t4 == 2) h |= H_MKT;    // type_4_interpretation MKT: the limit handlers' price overrides
+    if (h & (H_DISCARD | H_NEG1 | H_PM1 | H_MKT)) h |= H_RARE;
     x.x = h;
     x.y = sd;
 }
@@ -1005,12 +1011,17 @@ DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5,
     const i32 kind = h & H_KIND;
     if (kind == H_CNL_ASK) cancel<G, true, RC>(B, B.a, m);
     else if (kind == H_CNL_BID) cancel<G, false, RC>(B, B.b, m);
-    else if (kind == H_BID) bid_lim<G>(B, m);
-    else if (kind == H_ASK) ask_lim<G>(B, m);
+    else if (kind == H_BID) {
+        if (!G && !(h & H_RARE)) bid_lim<G, false>(B, m);
+        else bid_lim<G, true>(B, m);
+    } else if (kind == H_ASK) {
+        if (!G && !(h & H_RARE)) ask_lim<G, false>(B, m);
+        else ask_lim<G, true>(B, m);
+    }
 }
 template <bool RC, int S>
 DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
-    if (B.fl & F_FAST) process_msg_<false, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
+    if ((i32)B.fl < 0) process_msg_<false, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);  // F_FAST
     else process_msg_<true, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
 }
 // forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
