@@ -2120,7 +2120,12 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     } else {
         key = Key{keys[2 * e], keys[2 * e + 1]};
     }
-    const int ag = l - 32;
+    // partitionable keys and <= 16 agents: agent ag's randint takes two lanes, 32 + ag (the high
+    // word's key, split(k_ag)[0]) and 48 + ag (the low word's, split(k_ag)[1]), so levels 3 and 4
+    // below are one threefry per lane each (5 per step instead of 8; the chain depth is the same)
+    const bool two = part && c.n_agents <= 16 && A <= 32;
+    const bool hi_lane = two && l >= 48;
+    const int ag = l - (hi_lane ? 48 : 32);
     int t = 0, i = 0;
     agent_of_lane(c, ag < 0 ? 0 : ag, t, i);
     const bool agent_lane = (ag >= 0) & (ag < c.n_agents);
@@ -2131,6 +2136,23 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     o.next_master = nm;
     o.k1 = Key{(u32)rdl((i32)L1.a, 0), (u32)rdl((i32)L1.b, 0)};
     o.key_reset = Key{(u32)rdl((i32)L1.a, 1), (u32)rdl((i32)L1.b, 1)};
+    if (two) {
+        const Key P2 = from_lane(L1, agent_lane ? 2 + t : 0);
+        const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
+        // L3: lane 0 sub = split(sk)[1]; lane 32 + ag split(k_ag)[0]; lane 48 + ag split(k_ag)[1]
+        const Key L3 = split_key(L2, 2, ((l == 0) | hi_lane) ? 1 : 0, part);
+        // L4: lanes < A random_bits(sub, A)[l]; agent lanes random_bits(their key, 1)[0]
+        const Key sub = from_lane(L3, 0);
+        const u32 bits = random_bits(l < A ? sub : L3, 1, l < A ? l : 0, part);
+        o.shuffle_bits = bits;
+        const u32 hb = bits, lb = (u32)__builtin_amdgcn_ds_bpermute(((l + 16) & 63) << 2, (i32)bits);
+        const i32 na = agent_lane ? (MD ? action_hi(c.types[t]) : c.types[t].n_actions) : 1;
+        const u32 span = na <= 0 ? 1u : (u32)na;
+        u32 mult = 65536u % span;
+        mult = (mult * mult) % span;
+        o.acts = (i32)(((hb % span) * mult + (lb % span)) % span);
+        return o;
+    }
     // L2: lane 0 sk = split(k1)[1]; agent lanes: split(sub_t, n_agents_t)[i]
     const Key P2 = from_lane(L1, agent_lane ? 2 + t : 0);
     const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
