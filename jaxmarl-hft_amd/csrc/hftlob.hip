@@ -1837,31 +1837,36 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     TradeView<S> V;
     trade_view(B, V, false, -1, ovr0);
     const i32 inv = st[2];
-    i32 bqs = 0, sqs = 0;
-#pragma unroll
-    for (int r = 0; r < S; ++r) {
-        const bool mine = (tid == V.PT[r]) || (tid == V.AT[r]);
-        const i32 aQ = mine ? V.Q[r] : 0, apt = mine ? V.PT[r] : 0, aat = mine ? V.AT[r] : 0;
-        const bool buy = (aQ >= 0 && tid == apt) || (aQ < 0 && tid == aat);
-        const bool sel = (aQ < 0 && tid == apt) || (aQ >= 0 && tid == aat);
-        bqs = wadd(bqs, buy ? iabs_(aQ) : 0);
-        sqs = wadd(sqs, sel ? iabs_(aQ) : 0);
-    }
-    bqs = wave_sum(bqs);
-    sqs = wave_sum(sqs);
-    const i32 inv_b = wsub(wadd(inv, bqs), sqs);
     const i32 M = c.n_msgs;
-    i32 pen = wmul(tc.unwind_price_penalty, c.tick_size);
-    pen = inv_b > 0 ? pen : wsub(0, pen);
-    i32 unwind_px;
-    if (tc.unwind_price == HFTLOB_PRICE_FAR_TOUCH) unwind_px = wsub(sel(inv_b > 0, X.last_bb, X.last_ba), pen);
-    else unwind_px = f2i(self(tc.unwind_price == HFTLOB_PRICE_MID_AVG, X.avg_mid, X.last_mid) - i2f(pen));
-    const bool add = X.ep_done && iabs_(inv_b) > 0;
-    const i32 ovr[8] = {unwind_px, wmul(isign(inv_b), iabs_(inv_b)), c.artificial_order_id, c.placeholder_order_id,
-                        0, 0, c.artificial_trader_id, tid};
-    const int e = add ? first_any_neg1_trade(B) : -1;
-    trade_view(B, V, add, e, ovr);
-    R.forced_unwind = wmul(inv_b, (i32)X.ep_done);
+    // the forced unwind exists only on an episode's last step: the pre-unwind inventory and the
+    // second trade view are skipped on every other step (forced_unwind = inv_b * ep_done = 0)
+    R.forced_unwind = 0;
+    if (X.ep_done) {
+        i32 bqs = 0, sqs = 0;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const bool mine = (tid == V.PT[r]) || (tid == V.AT[r]);
+            const i32 aQ = mine ? V.Q[r] : 0, apt = mine ? V.PT[r] : 0, aat = mine ? V.AT[r] : 0;
+            const bool buy = (aQ >= 0 && tid == apt) || (aQ < 0 && tid == aat);
+            const bool sel = (aQ < 0 && tid == apt) || (aQ >= 0 && tid == aat);
+            bqs = wadd(bqs, buy ? iabs_(aQ) : 0);
+            sqs = wadd(sqs, sel ? iabs_(aQ) : 0);
+        }
+        bqs = wave_sum(bqs);
+        sqs = wave_sum(sqs);
+        const i32 inv_b = wsub(wadd(inv, bqs), sqs);
+        i32 pen = wmul(tc.unwind_price_penalty, c.tick_size);
+        pen = inv_b > 0 ? pen : wsub(0, pen);
+        i32 unwind_px;
+        if (tc.unwind_price == HFTLOB_PRICE_FAR_TOUCH) unwind_px = wsub(sel(inv_b > 0, X.last_bb, X.last_ba), pen);
+        else unwind_px = f2i(self(tc.unwind_price == HFTLOB_PRICE_MID_AVG, X.avg_mid, X.last_mid) - i2f(pen));
+        if (iabs_(inv_b) > 0) {
+            const i32 ovr[8] = {unwind_px, wmul(isign(inv_b), iabs_(inv_b)), c.artificial_order_id,
+                                c.placeholder_order_id, 0, 0, c.artificial_trader_id, tid};
+            trade_view(B, V, true, first_any_neg1_trade(B), ovr);
+        }
+        R.forced_unwind = inv_b;
+    }
     // post-unwind stats
     const int ri = tc.reference_price;
     const bool ref_int = ri == HFTLOB_PRICE_FAR_TOUCH || ri == HFTLOB_PRICE_NEAR_TOUCH;
@@ -2000,30 +2005,35 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     trade_view(B, V, false, -1, ovr0);
     const i32 task = st[1], qe = st[2], sell = st[3];
     const float init_price = bitf(st[0]);
-    i32 qsum = 0;
+    // the fictional doom trade exists only on an episode's last step: the pre-unwind quantity and
+    // the second trade view are skipped on every other step (doom_quant = ep_done * quant_left = 0)
+    R.doom_quant = 0;
+    if (X.ep_done) {
+        i32 qsum = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) qsum = wadd(qsum, (tid == V.PT[r] || tid == V.AT[r]) ? V.Q[r] : 0);
-    const i32 qets = iabs_(wave_sum(qsum));
-    const i32 quant_left = wsub(task, wadd(qe, qets));
-    const i32 pen = wmul(tc.doom_price_penalty, tick);
-    const i32 side_sign = wsub(wmul(sell, 2), 1);
-    i32 refp;
-    const float penf = tc.doom_penalty_is_float ? tc.doom_penalty_f32 : i2f(pen);
-    if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH && !tc.doom_penalty_is_float)
-        refp = sell ? wmul(ifloordiv(wsub(X.last_bb, pen), tick), tick)
-                    : wmul(ifloordiv(wadd(X.last_ba, pen), tick), tick);
-    else if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)  // int32 price - Python float: f32
-        refp = sell ? f2i(ffloordiv(i2f(X.last_bb) - penf, (float)tick) * (float)tick)
-                    : f2i(ffloordiv(i2f(X.last_ba) + penf, (float)tick) * (float)tick);
-    else
-        refp = sell ? f2i(ffloordiv(X.avg_mid - penf, (float)tick) * (float)tick)
-                    : f2i(ffloordiv(X.avg_mid + penf, (float)tick) * (float)tick);
-    const bool add = X.ep_done && quant_left > 0;
-    const i32 ovr[8] = {refp, wmul(side_sign, iabs_(quant_left)), c.artificial_order_id, c.placeholder_order_id,
-                        0, 0, c.artificial_trader_id, tid};
-    const int e = add ? first_any_neg1_trade(B) : -1;
-    trade_view(B, V, add, e, ovr);
-    R.doom_quant = wmul((i32)X.ep_done, quant_left);
+        for (int r = 0; r < S; ++r) qsum = wadd(qsum, (tid == V.PT[r] || tid == V.AT[r]) ? V.Q[r] : 0);
+        const i32 qets = iabs_(wave_sum(qsum));
+        const i32 quant_left = wsub(task, wadd(qe, qets));
+        const i32 pen = wmul(tc.doom_price_penalty, tick);
+        const i32 side_sign = wsub(wmul(sell, 2), 1);
+        i32 refp;
+        const float penf = tc.doom_penalty_is_float ? tc.doom_penalty_f32 : i2f(pen);
+        if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH && !tc.doom_penalty_is_float)
+            refp = sell ? wmul(ifloordiv(wsub(X.last_bb, pen), tick), tick)
+                        : wmul(ifloordiv(wadd(X.last_ba, pen), tick), tick);
+        else if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)  // int32 price - Python float: f32
+            refp = sell ? f2i(ffloordiv(i2f(X.last_bb) - penf, (float)tick) * (float)tick)
+                        : f2i(ffloordiv(i2f(X.last_ba) + penf, (float)tick) * (float)tick);
+        else
+            refp = sell ? f2i(ffloordiv(X.avg_mid - penf, (float)tick) * (float)tick)
+                        : f2i(ffloordiv(X.avg_mid + penf, (float)tick) * (float)tick);
+        if (quant_left > 0) {
+            const i32 ovr[8] = {refp, wmul(side_sign, iabs_(quant_left)), c.artificial_order_id,
+                                c.placeholder_order_id, 0, 0, c.artificial_trader_id, tid};
+            trade_view(B, V, true, first_any_neg1_trade(B), ovr);
+        }
+        R.doom_quant = quant_left;
+    }
     i32 aq = 0, oq = 0, qp = 0;
     float dur[S];
 #pragma unroll
@@ -2216,6 +2226,11 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
     fetch_side(fa, rec + c.off_asks, B.vs);
     fetch_side(fb, rec + c.off_bids, B.vs);
+    // the agent states (<= 64 words: one per lane), loaded with the book: the agent and reward
+    // phases read them with v_readlane instead of waiting on scalar loads per agent
+    const int naw = c.rec_words - c.off_agents;
+    const bool agw_pre = naw <= 64;
+    const i32 agw = (agw_pre & (l < naw)) ? rec[c.off_agents + l] : 0;
     const StepKeys SK = step_keys<NFIX == 0>(c, key_n, ek, keys, master, mk);
     if (master) mk = SK.next_master;
     const Key key_reset = SK.key_reset;
@@ -2264,7 +2279,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
 #ifdef HFTLOB_STAMPS
-    unsigned long long acc_act = 0, acc_cnl = 0, acc_flt = 0;
+    unsigned long long acc_act = 0, acc_cnl = 0, acc_flt = 0, acc_mmr = 0, acc_exr = 0, acc_obs = 0;
 #endif
     {
         int ag = 0, arow = C, crow = 0, aw = 0;
@@ -2299,7 +2314,12 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     for (int j = 0; j < 4; ++j) av[j] = rdl(v, j);
                     act = av[0];
                 }
-                i32 s4[4] = {st[0], st[1], st[2], st[3]};
+                i32 s4[4];
+                {
+                    const int b = (int)(st - (rec + c.off_agents));
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) s4[k] = agw_pre ? rdl(agw, b + k) : st[k];
+                }
                 ActX x{0, 0, 0, 0, 0, 0};
                 STAMP(ta0);
                 if (tc.kind == HFTLOB_AGENT_MM) {
@@ -2478,7 +2498,10 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 const i32 tid = wsub(tc.trader_id0, i);
                 const int nw = agent_words(tc);
                 i32 s[13];
-                for (int k = 0; k < 13; ++k) s[k] = k < nw ? st[k] : 0;
+                {
+                    const int b = (int)(st - (rec + c.off_agents));
+                    for (int k = 0; k < 13; ++k) s[k] = k < nw ? (agw_pre ? rdl(agw, b + k) : st[k]) : 0;
+                }
                 i32 d = 0;
                 float rew;
                 i32 iw[HFTLOB_INFO_AGENT_WORDS];
@@ -2487,9 +2510,11 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 ax1.bid_price = uni(axs[ag * 6 + 0]); ax1.ask_price = uni(axs[ag * 6 + 1]);
                 ax1.bid_dist = uni(axs[ag * 6 + 2]); ax1.ask_dist = uni(axs[ag * 6 + 3]);
                 ax1.bid_quant = uni(axs[ag * 6 + 4]); ax1.ask_quant = uni(axs[ag * 6 + 5]);
+                STAMP(tr0);
                 if (tc.kind == HFTLOB_AGENT_MM) {
                     MMRew R;
                     mm_reward(c, tc, B, X, s, tid, excl_any, R);
+                    STAMP_ACC(acc_mmr, tr0);
                     const float tot = bitf(s[3]) + R.PnL;
                     s[0] = ax1.bid_dist; s[1] = ax1.ask_dist; s[2] = R.end_inventory; s[3] = fbit(tot);
                     s[4] = fbit(R.cash);
@@ -2506,6 +2531,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 } else {
                     EXRew R;
                     exe_reward(c, tc, B, X, s, tid, R);
+                    STAMP_ACC(acc_exr, tr0);
                     s[2] = wadd(s[2], R.agentQuant);
                     s[4] = fbit(R.p_vwap);
                     s[5] = fbit(bitf(s[5]) + i2f(R.qp_agent));
@@ -2528,6 +2554,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     for (int k = 0; k < HFTLOB_INFO_AGENT_WORDS; ++k) if (l == k) v = iw[k];
                     if (l < HFTLOB_INFO_AGENT_WORDS) info[HFTLOB_INFO_WORLD_WORDS + ag * HFTLOB_INFO_AGENT_WORDS + l] = v;
                 }
+                STAMP(to0);
                 if (!all) {  // stepped state + obs survive only when the episode continues
                     i32 v = 0;
                     for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
@@ -2537,6 +2564,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 if (obs_raw_out)  // the stepped state's raw obs, also on an episode's last step (info)
                     write_obs<true>(c, tc, wv, s, obs_raw_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, false,
                                     ftime);
+                STAMP_ACC(acc_obs, to0);
                 st += nw;
             }
         }
@@ -2562,6 +2590,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         info[5] = (i32)(t_keys - t_start); info[6] = (i32)(t_load - t_keys); info[7] = (i32)(t_rows - t_load);
         info[8] = (i32)(t_agents - t_rows);
         info[9] = (i32)acc_act; info[10] = (i32)acc_cnl; info[11] = (i32)acc_flt;
+        info[12] = (i32)acc_mmr; info[13] = (i32)acc_exr; info[14] = (i32)acc_obs;
     }
 #endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs

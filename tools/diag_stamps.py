@@ -35,14 +35,15 @@ rows = []
 for k in range(80):
     env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)   # the bench's path
     if k >= 8:
-        rows.append(env._out["info"][:, :12].cpu().numpy().copy())
+        rows.append(env._out["info"][:, :15].cpu().numpy().copy())
 r = np.concatenate(rows).astype(np.int64)
 names = ["setup+agent msgs+shuffle", "112-msg book loop", "rewards+state+obs", "store+info"]
 tot = r[:, :4].sum(1)
 print(f"env-steps sampled: {len(r)}; median total cycles/env-step: {np.median(tot):.0f}")
 for i, n in enumerate(names):
     print(f"  {n:28s} median {np.median(r[:, i]):9.0f}  mean {r[:, i].mean():9.0f}  share {r[:, i].sum() / tot.sum():.3f}")
-for i, n in zip(range(5, 12), ["  setup: step keys (PRNG)", "  setup: load book sides", "  setup: agent rows",
+for i, n in zip(range(5, 15), ["  setup: step keys (PRNG)", "  setup: load book sides", "  setup: agent rows",
                               "  setup: ids + shuffle", "    agents: action msgs", "    agents: cancel rows",
-                              "    agents: filter"]):
+                              "    agents: filter", "  rewards: MM reward", "  rewards: EXE reward",
+                              "  rewards: state + obs writes"]):
     print(f"  {n:28s} median {np.median(r[:, i]):9.0f}  mean {r[:, i].mean():9.0f}")
