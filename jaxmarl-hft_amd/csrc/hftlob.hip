@@ -2430,11 +2430,17 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         decode_msgs(B.c, x, y);
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
         const int cnt = uni(imin_(64, M - base));  // SGPR: the loop test stays on the scalar unit
+        // message k + 1's fields are read (v_readlane) at the end of message k, so their latency
+        // overlaps the best-quote record and the loop test instead of stalling the dispatch
+        i32 h = rdl(x.x, 0), d1 = rdl(x.y, 0), d2 = rdl(x.z, 0), d3 = rdl(x.w, 0), d4 = rdl(y.x, 0),
+            d5 = rdl(y.y, 0), d6 = rdl(y.z, 0), d7 = rdl(y.w, 0);
         for (int k = 0; k < cnt; ++k) {
             if (RC) B.mi = base + k;
-            process_msg<RC>(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
-                            rdl(y.z, k), rdl(y.w, k));
+            process_msg<RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
             refresh_best(B);
+            const int kn = (k + 1) & 63;
+            h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
+            d4 = rdl(y.x, kn); d5 = rdl(y.y, kn); d6 = rdl(y.z, kn); d7 = rdl(y.w, kn);
             rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
             rpb = wlane(rpb, B.b.best_p, k); rqb = wlane(rqb, B.b.best_q, k);
         }
