@@ -102,3 +102,18 @@ def test_reference_env_configs_pack(fname):
     c, L = pack_env_cfg(cfg, 4, 100_000, True)
     assert c.n_msgs == L.n_msgs and c.n_types == len(cfg.dict_of_agents_configs)
     assert c.action_words == sum(c.types[t].n_agents * c.types[t].action_width for t in range(c.n_types))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CFG_DIR), reason="reference configs not mounted")
+def test_reference_env_config_fixture_is_current():
+    """tests/golden/reference_env_configs.json (what the GPU run test steps) is the reference's
+    config/env_configs as our loader reads them."""
+    import json
+    from dataclasses import asdict
+    from hftlob.config_io import load_config_from_file
+    with open(os.path.join(os.path.dirname(__file__), "golden", "reference_env_configs.json")) as f:
+        fix = json.load(f)
+    names = sorted(n for n in os.listdir(REF_CFG_DIR) if n.endswith(".json"))
+    assert sorted(fix) == names
+    for n in names:
+        assert json.loads(json.dumps(asdict(load_config_from_file(os.path.join(REF_CFG_DIR, n))))) == fix[n], n

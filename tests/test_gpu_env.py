@@ -541,3 +541,21 @@ def test_speed_test_sweep_parity(agents, D):
                                     env._init_states.cpu().numpy(), s0, T)
     _compare_state(env, o_st, state.buf.cpu().numpy(), "rollout_sampled")
     assert (k_out.cpu().numpy().view(np.uint32) == o_key).all(), "carried key"
+
+
+def _ref_configs():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(__file__), "golden", "reference_env_configs.json")
+    with open(p) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("fname", sorted(_ref_configs()))
+def test_reference_env_config_runs(fname):
+    """Every env config the reference ships (config/env_configs/*.json, serialised into
+    tests/golden/reference_env_configs.json by tests/golden/make_reference_env_configs.py) runs on
+    the HIP env and matches the oracle over 24 steps."""
+    from hftlob.config_io import dict_to_multiagent_config
+    cfg = dict_to_multiagent_config(_ref_configs()[fname])
+    rollout_parity(cfg, E=16, K=24)
