@@ -128,3 +128,39 @@ def test_learner_on_device_matches_numpy():
             upd = lr * (m / 0.1) / (np.sqrt(v / 0.001) + 1e-5)
             want_p = p_ref.detach().numpy() - upd
             assert np.allclose(npy(p_dev), want_p, rtol=1e-5, atol=lr * 2e-3), f"type {i}: {name} after one step"
+
+
+def test_trainer_update_over_rccl_world1():
+    """The multi-rank learner path (gradient pmean through torch.distributed) on the RCCL backend
+    ("nccl" on ROCm), world_size 1 on the box's one GPU: the update runs with the collective in
+    it and matches a trainer without a process group (the pmean of one rank is the identity)."""
+    import socket
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cfg = builtin_config("2_player_fq_fqc")
+    w = cfg.world_config
+    day = generate_day(n_msgs=30_000, seed=4, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    c = lambda: I.default_config(NUM_ENVS=64, NUM_STEPS=8, GRU_HIDDEN_DIM=16, FC_DIM_SIZE=16,  # noqa: E731
+                                 NUM_MINIBATCHES=2, UPDATE_EPOCHS=1, TOTAL_TIMESTEPS=64 * 8 * 4)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        # the bucketed all-reduce itself runs over RCCL (the trainer skips it at world_size 1)
+        g = torch.nn.Parameter(torch.zeros(5, device="cuda"))
+        g.grad = torch.arange(5, dtype=torch.float32, device="cuda")
+        I._average_grads([g], dist)
+        torch.cuda.synchronize()
+        assert torch.equal(g.grad, torch.arange(5, dtype=torch.float32, device="cuda"))
+        env1 = MARLEnv(None, cfg, data=day, return_info=False, persistent_outputs=True)
+        tr1 = I.IPPOTrainer(env1, c(), dist=dist)
+        tr1.update()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    env0 = MARLEnv(None, cfg, data=day, return_info=False, persistent_outputs=True)
+    tr0 = I.IPPOTrainer(env0, c())
+    tr0.update()
+    for n1, n0 in zip(tr1.nets, tr0.nets):
+        for a, b in zip(n1.parameters(), n0.parameters()):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
