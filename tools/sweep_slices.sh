@@ -1,8 +1,8 @@
-# A/B of MARLEnv.rollout_sampled env slices (bench.py --slices) on one GPU.
+# A/B of MARLEnv.rollout_sampled launch shapes (bench.py --slices) on one GPU: 0 = one persistent
+# k_env_rollout launch (every env's steps back to back), 1..4 = env slices on their own streams.
 set -o pipefail
-mkdir -p gpurun_out/sweep
-timeout -k 10 300 python -u -m pytest tests/test_gpu_env.py -k "rollout_sampled" -x -q --timeout 120 --timeout-method thread > gpurun_out/sweep/tests.log 2>&1 || exit 3
-for G in 2 3 4; do
-  timeout -k 10 120 python bench.py --no-cpu-baseline --steps 128 --slices $G > gpurun_out/sweep/G$G.json 2> gpurun_out/sweep/G$G.err || exit 4
-done
-timeout -k 10 120 python bench.py --no-cpu-baseline --steps 512 --slices 2 > gpurun_out/sweep/G2_512.json 2> gpurun_out/sweep/G2_512.err || exit 5
+O=gpurun_out/${1:-sweep}
+mkdir -p $O
+for r in 1 2; do for G in 0 1 2 3 4; do
+  timeout -k 10 120 python bench.py --no-cpu-baseline --steps 128 --slices $G > $O/G${G}_$r.json 2> $O/G$G.err || exit 4
+done; done
