@@ -332,6 +332,11 @@ struct Side {
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid under F_OK
     i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
                          // every handler reads prices, only adds and row clears write them
+    // top-of-book cache: the slot _get_top_*_order_idx returns for max / min price top_p, and its
+    // (ts, tns); top = -1: unknown.  Kept across messages: a quantity change keeps it, clearing the
+    // row (or any bulk clear) drops it, an add at a better price or an earlier time at top_p
+    // replaces it (see top_new / top_eq), so a crossing message usually skips the top-of-book scan
+    i32 top, top_p, top_ts, top_tns;
 };
 
 // slot e of a lane-strided register column <- v (lane e & 63 of register e >> 6): one
@@ -401,14 +406,15 @@ template <bool ASKS, int S> DEV u32 commit_side(Side<S>& s, const SideRows<S>& f
             t[FP * R] = p; t[FQ * R] = q; t[FOID * R] = oid; t[FTID * R] = tid; t[FTS * R] = ts; t[FTNS * R] = tns;
         }
         s.pc[r] = V.v[r] ? p : -1;
-        const u32 np = ~(u32)p, nq = ~(u32)q, no = ~(u32)oid, nt = ~(u32)tid, ns = ~(u32)ts, nn = ~(u32)tns;
-        const u32 any0 = min(min(min(np, nq), min(no, nt)), min(ns, nn));  // 0 <=> some field == -1
-        const u32 all0 = max(max(max(np, nq), max(no, nt)), max(ns, nn));  // 0 <=> every field == -1
+        const u32 np_ = ~(u32)p, nq = ~(u32)q, no = ~(u32)oid, nt = ~(u32)tid, ns = ~(u32)ts, nn = ~(u32)tns;
+        const u32 any0 = min(min(min(np_, nq), min(no, nt)), min(ns, nn));  // 0 <=> some field == -1
+        const u32 all0 = max(max(max(np_, nq), max(no, nt)), max(ns, nn));  // 0 <=> every field == -1
         bad |= V.m[r] & bal((q <= 0) & (all0 != 0u));
         n1 |= V.m[r] & bal((p != -1) & (any0 == 0u));
         pm1 |= V.m[r] & bal((p == -1) & (all0 != 0u));
     }
     lds_order();
+    s.top = -1;
     return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u) |
            (pm1 != 0ull ? SideBits<ASKS>::PM1 : 0u);
 }
@@ -444,6 +450,7 @@ template <int S> DEV void clear_masked(Side<S>& s, int R, const lmask (&m)[S]) {
         }
     }
     lds_order();
+    s.top = -1;
 }
 
 // _removeZeroNegQuant — JaxOrderBookArrays.py:85-90 on a side that is not
@@ -606,35 +613,54 @@ struct Msg {
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
 // side: it changes (best_p, best_q) only where get_best_* / get_volume_at_price
 // would, and falls back to a full recompute (ok = false) where it cannot tell.
-template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq, i32 maxint) {
-    // an all -1 row now holds (np, nq > 0).  Branches ordered for the common case, an order
-    // behind the best (one compare each); per side the cases are those of get_best_* with -1
-    // (and, for asks, maxint) standing for "no price".
+// the top-of-book cache after an order (np, t, tns) went to slot e:
+// a new best price: the row is alone at it, so it is the top (unless a maxint time, where the
+// top-of-book formula's maxint placeholders could tie with it)
+template <int S> DEV void top_new(Side<S>& s, int e, i32 np, i32 t, i32 tns, i32 maxint) {
+    s.top = ((t != maxint) & (tns != maxint)) ? e : -1;
+    s.top_p = np; s.top_ts = t; s.top_tns = tns;
+}
+// an order at the best price: the top moves to it only if it is earlier in (ts, tns, slot)
+template <int S> DEV void top_eq(Side<S>& s, int e, i32 np, i32 t, i32 tns, i32 maxint) {
+    if (s.top < 0 || np != s.top_p || t > s.top_ts) return;  // (the common case: a later order)
+    if (t < s.top_ts || tns < s.top_tns || (tns == s.top_tns && e < s.top)) {
+        s.top = tns != maxint ? e : -1;  // (t < top_ts < maxint)
+        s.top_ts = t; s.top_tns = tns;
+    }
+}
+template <bool BID, int S>
+DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint) {
+    // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
+    // common case, an order behind the best (one compare each); per side the cases are those of
+    // get_best_* with -1 (and, for asks, maxint) standing for "no price".
     constexpr u32 OK = SideBits<!BID>::OK;
-    if (!(fl & OK)) return;
+    if (!(fl & OK)) { s.top = -1; return; }
     const i32 bp = s.best_p;
     if (BID) {
         if (np < bp) {
             if (bp == -1) fl &= ~OK;        // np < -1 on an empty side
         } else if (np > bp) {
             s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
+            top_new(s, e, np, t, tns, maxint);
         } else if (bp == -1) {
             fl &= ~OK;                      // np == -1 on an empty side
         } else {
             s.best_q = wadd(s.best_q, nq);
+            top_eq(s, e, np, t, tns, maxint);
         }
     } else {
         if (np > bp) {
             if (bp == -1) {                 // empty side
                 if (np == maxint) fl &= ~OK;
-                else { s.best_p = np; s.best_q = nq; }
+                else { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
             }
         } else if (np < bp) {
-            if (np != -1) { s.best_p = np; s.best_q = nq; }
+            if (np != -1) { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
         } else if (np == -1) {
             fl &= ~OK;
         } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
+            top_eq(s, e, np, t, tns, maxint);
         }
     }
 }
@@ -664,6 +690,7 @@ template <int S> DEV void side_put(Side<S>& s, int R, int e, i32 f0, i32 f1, i32
 template <int S> DEV void side_clr(Side<S>& s, int R, int e) {
     clr6(s.t, s.scr, R, e);
     col_set(s.pc, e, -1);
+    s.top = e == s.top ? -1 : s.top;
 }
 // the side's p == -1 slots (all -1 rows in the FAST variant)
 template <int S> DEV void free_slots(const Book<S>& B, const Side<S>& s, lmask (&free)[S]) {
@@ -741,13 +768,24 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
         } else if (mp < price) {
             break;
         }
-        i32 q[S], o[S], t[S], ts[S], tn[S];
-        ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
-        ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
-        const int top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
+        int top;
+        i32 qt, ot, tt;
+        if (s.top >= 0 && s.top_p == mp) {  // the cached top: three broadcast reads
+            top = s.top;
+            qt = ldu(s.t, R, FQ, top); ot = ldu(s.t, R, FOID, top); tt = ldu(s.t, R, FTID, top);
+        } else {
+            i32 q[S], o[S], t[S], ts[S], tn[S];
+            ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
+            ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
+            top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
+            qt = sget(q, top); ot = sget(o, top); tt = sget(t, top);
+            const i32 tts = sget(ts, top), ttn = sget(tn, top);
+            s.top_p = mp; s.top_ts = tts; s.top_tns = ttn;
+            s.top = ((mp != -1) & (mp != B.c.maxint) & (tts != B.c.maxint) & (ttn != B.c.maxint)) ? top : -1;
+        }
         const i32 tp = sget(s.pc, top);
         if (!((BID ? tp >= price : tp <= price) && tp != -1)) break;
-        qtm = match_order<G, !BID>(B, s, top, qtm, m, sget(q, top), tp, sget(o, top), sget(t, top));
+        qtm = match_order<G, !BID>(B, s, top, qtm, m, qt, tp, ot, tt);
     }
     return qtm;
 }
@@ -766,8 +804,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         if (nq > 0) {
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
             if (m.h & (H_NEG1 | H_PM1)) B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
-            if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
-            else B.fl &= ~OK;
+            if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
+            else { B.fl &= ~OK; s.top = -1; }
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
             side_clr(s, R, e);
             B.fl &= ~OK;
@@ -802,8 +840,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         if (m.h & H_NEG1) B.fl |= NEG1;
         if (m.h & H_PM1) B.fl |= PM1;
-        if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
-        else B.fl &= ~OK;
+        if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
+        else { B.fl &= ~OK; s.top = -1; }
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         side_clr(s, R, e);
         B.fl &= ~OK;
@@ -826,8 +864,12 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
     lmask m[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(s.pc[r] == worst);
+    const i32 top = s.top;
     clear_masked(s, R, m);
-    B.fl &= ~SideBits<!BID>::OK;
+    // only the worst level goes: the best quote and the top of book survive unless the side holds
+    // one price level (worst == best; an ask side whose prices are all maxint has best -1)
+    s.top = worst != s.top_p ? top : -1;
+    if ((worst == s.best_p) | (s.best_p == -1)) B.fl &= ~SideBits<!BID>::OK;
     free_slots(B, s, free);
 }
 // The common add: FAST book, a free (all -1) slot exists, no eviction: the order goes to the
@@ -847,7 +889,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
     }
-    note_add<BID>(s, B.fl, m.price, qty, B.c.maxint);
+    note_add<BID>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
@@ -966,6 +1008,12 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
         }
     }
     const i32 op = sget(s.pc, idx), oq = sget(q, idx);
+    // FAST sides: a p == -1 row holds -1 in every field but q (a cancel of a negative quantity can
+    // leave q > 0 there).  Cancelling qty >= -1 from an all -1 row leaves q = -1 - qty <= 0, which
+    // _removeZeroNegQuant clears back to all -1: the book and its best quotes are unchanged.  This
+    // is the common cancel of the replayed data (an order id the episode's book does not hold, no
+    // init-id match: the -1 index wraps to the last slot, usually empty; tools/msg_mix.py).
+    if (!G && ((op & oq) == -1) && m.qty >= -1) return;
     const i32 nq = wsub(oq, m.qty);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (nq <= 0) side_clr(s, R, idx);
@@ -2212,6 +2260,9 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                       i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
                       i32* lds) {
     STAMP(t_start);
+#ifdef HFTLOB_STAMPS
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the in-kernel clock
+#endif
     const int l = lane_id();
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
     i32* rec = state + (size_t)e * c.rec_words;
@@ -2597,6 +2648,7 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         info[8] = (i32)(t_agents - t_rows);
         info[9] = (i32)acc_act; info[10] = (i32)acc_cnl; info[11] = (i32)acc_flt;
         info[12] = (i32)acc_mmr; info[13] = (i32)acc_exr; info[14] = (i32)acc_obs;
+        info[15] = (i32)(__builtin_amdgcn_s_memrealtime() - rt_start);
     }
 #endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
@@ -2838,6 +2890,16 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
     return launch_status();
 }
 
+// dynamic LDS of one env's workgroup: [agent rows][action extras][book] (see env_step_dev)
+#ifndef HFTLOB_LDS_FLOOR
+#define HFTLOB_LDS_FLOOR 0
+#endif
+static size_t env_shm(const hftlob_env_cfg* cfg) {
+    const size_t b = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
+                          12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+    return b < (size_t)HFTLOB_LDS_FLOOR ? (size_t)HFTLOB_LDS_FLOOR : b;
+}
+
 static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int key_n, const uint32_t* keys,
                            const uint32_t* key_in, uint32_t* key_out, int32_t* actions, const int32_t* msg_data,
                            const int32_t* init_states, int32_t* state, const hftlob_step_out* out, void* stream) {
@@ -2845,8 +2907,7 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
-    const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
-                            12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+    const size_t shm = env_shm(cfg);
 #define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, keys, \
                                                key_in, key_out, actions, msg_data, init_states, state, *out)
     if (cfg->lob.cancel_mode >= 2) {  // random cancel fallback: general sizes only
@@ -2870,8 +2931,7 @@ static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, 
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
-    const size_t shm = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
-                            12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+    const size_t shm = env_shm(cfg);
 #define LAUNCH_ROLL(SS, NF, RC) hipLaunchKernelGGL((k_env_rollout<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, \
                                                n_steps, per_step, key_in, key_out, actions, msg_data, init_states, \
                                                state, *out)

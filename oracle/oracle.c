@@ -285,6 +285,10 @@ static void cancel_order(const hftlob_lob_cfg* c, i32* s, const Msg* m, const u3
             if (idx == -1 && c->cancel_mode == 3) idx = random_id_match(c, k, s, m, 1);
         }
     }
+#ifdef ORACLE_STATS
+    if (m->qty != 0 && idx >= 0 && s[idx * 6 + 2] != m->oid) STAT(21);   /* init-id fallback found */
+    if (m->qty != 0 && idx == -1) { STAT(22); if (s[(nO - 1) * 6] == -1) STAT(23); }
+#endif
     if (idx == -1) idx = nO - 1; /* negative index wraps to the last slot */
 #ifdef ORACLE_STATS
     if (m->qty != 0) {
@@ -343,6 +347,9 @@ static i32 match_order(i32* s, int nO, int top, i32 qtm, const Msg* m, i32* trad
     i32* r = s + top * 6;
     i32 newq = imax(0, wsub(r[1], qtm));
     i32 rem = wsub(qtm, r[1]);
+#ifdef ORACLE_STATS
+    if (newq <= 0) STAT(24);
+#endif
     int e = nT - 1;
     for (int i = 0; i < nT; ++i)
         if (trades[i * 8 + 4] == -1) { e = i; break; }
@@ -378,6 +385,9 @@ static void bid_lim(const hftlob_lob_cfg* c, Msg m, i32* asks, i32* bids, i32* t
         int full = 1;
         i32 worst = bids[0];
         for (int i = 0; i < nO; ++i) { full &= bids[i * 6] >= 0; worst = imin(worst, bids[i * 6]); }
+#ifdef ORACLE_STATS
+        if (full) STAT(25);
+#endif
         if (full)
             for (int i = 0; i < nO; ++i)
                 if (bids[i * 6] == worst) for (int f = 0; f < 6; ++f) bids[i * 6 + f] = -1;
@@ -396,6 +406,9 @@ static void ask_lim(const hftlob_lob_cfg* c, Msg m, i32* asks, i32* bids, i32* t
         int full = 1;
         i32 worst = asks[0];
         for (int i = 0; i < nO; ++i) { full &= asks[i * 6] >= 0; worst = imax(worst, asks[i * 6]); }
+#ifdef ORACLE_STATS
+        if (full) STAT(25);
+#endif
         if (full)
             for (int i = 0; i < nO; ++i)
                 if (asks[i * 6] == worst) for (int f = 0; f < 6; ++f) asks[i * 6 + f] = -1;

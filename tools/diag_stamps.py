@@ -35,11 +35,15 @@ rows = []
 for k in range(80):
     env.step_sampled(kbuf[k % 2], kbuf[(k + 1) % 2], state, params)   # the bench's path
     if k >= 8:
-        rows.append(env._out["info"][:, :15].cpu().numpy().copy())
+        rows.append(env._out["info"][:, :16].cpu().numpy().copy())
 r = np.concatenate(rows).astype(np.int64)
 names = ["setup+agent msgs+shuffle", "112-msg book loop", "rewards+state+obs", "store+info"]
 tot = r[:, :4].sum(1)
 print(f"env-steps sampled: {len(r)}; median total cycles/env-step: {np.median(tot):.0f}")
+# in-kernel clock (MI355X_MICROARCH.md DVFS item 6): shader cycles / 100 MHz realtime ticks, per wave-step
+clk = r[:, :4].sum(1) / np.maximum(r[:, 15], 1) * 100e6
+print(f"in-kernel clock: median {np.median(clk) / 1e9:.3f} GHz (p10 {np.percentile(clk, 10) / 1e9:.3f}, "
+      f"p90 {np.percentile(clk, 90) / 1e9:.3f}); median wave-step {np.median(r[:, 15]) * 10:.0f} ns")
 for i, n in enumerate(names):
     print(f"  {n:28s} median {np.median(r[:, i]):9.0f}  mean {r[:, i].mean():9.0f}  share {r[:, i].sum() / tot.sum():.3f}")
 for i, n in zip(range(5, 15), ["  setup: step keys (PRNG)", "  setup: load book sides", "  setup: agent rows",

@@ -14,7 +14,10 @@ NAMES = {0: "ask_lim", 1: "bid_lim", 2: "cancel ask", 3: "cancel bid", 4: "noop"
          6: "lim with qty <= 0", 7: "lim that crosses (>= 1 match)", 10: "cancels", 11: "cancel qty 0",
          12: "cancel found by oid", 13: "cancel removes the row", 14: "cancel at the best price",
          15: "best ask price changed", 16: "best bid price changed", 17: "best ask (p,q) changed",
-         18: "best bid (p,q) changed", 20: "match trips"}
+         18: "best bid (p,q) changed", 20: "match trips", 21: "cancel found by the init-id fallback",
+         22: "cancel of no row (wraps to the last slot)", 23: "... and the last slot is empty",
+         24: "match trips that empty the top order",
+         25: "limit order into a full side (check_book_fill eviction)"}
 
 
 def main():
