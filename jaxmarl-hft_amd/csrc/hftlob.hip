@@ -56,9 +56,21 @@ DEV i32 ifloordiv(i32 a, i32 b) {
     if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
     return q;
 }
+// fmodf, exactly, without the library's bit-by-bit reduction loop when |x / y| < 2^23 (prices
+// over a tick): with the correctly rounded quotient q' of |x| / |y| < 2^23, trunc(q') is the true
+// quotient Q or Q + 1 (Q and Q + 1 are floats and rounding is monotonic), so |x| - trunc(q')|y|
+// lies in [-|y|, |y|) and is a multiple of the smaller ulp: the fma computes it exactly, and adding
+// |y| back to a negative one is exact too.  NaN, inf, zero and huge quotients take fmodf.
+DEV float fmod_exact(float x, float y) {
+    const float ax = fabsf(x), ay = fabsf(y), qf = ax / ay;
+    if (!(qf < 8388608.0f) | !(ay > 0.0f) | !(ay < INFINITY)) return fmodf(x, y);
+    float r = fmaf(-truncf(qf), ay, ax);
+    r = r < 0.0f ? r + ay : r;
+    return copysignf(r, x);
+}
 // jnp.floor_divide for float32 (jax _float_divmod, round half away from zero)
 DEV float ffloordiv(float x, float y) {
-    float mod = fmodf(x, y);
+    float mod = fmod_exact(x, y);
     float div = (x - mod) / y;
     bool ind = (mod != 0.0f) && (((y > 0) - (y < 0)) != ((mod > 0) - (mod < 0)));
     if (ind) div = div - 1.0f;
