@@ -40,6 +40,7 @@ CONFIG = "2_player_fq_fqc"
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_CU, CLOCK_HZ = 256, 2.4e9    # MI355X CUs, max engine clock (MI355X_MICROARCH.md)
 CPU_STEPS = 64                 # CPU baseline / parity: one full episode (incl. the auto-reset)
+PROFILE = "r02_kernel_profile.json"  # profiles/: rocprof figures of the metric kernel (tools/profile_round.sh)
 
 
 def parse_args(argv=None):
@@ -58,7 +59,8 @@ def parse_args(argv=None):
                     help="rollout: one fused launch per step (key split + action sampling + step); "
                          "step: split_keys, sample_actions and env.step as three launches (SURVEY.md 8(d))")
     ap.add_argument("--slices", type=int, default=-1,
-                    help="rollout mode: env slices on streams of their own (1..4; -1 = MARLEnv.default_slices)")
+                    help="rollout mode: 0 = one persistent launch for all steps, 1..4 = env slices on streams "
+                         "of their own (-1 = MARLEnv.default_slices)")
     ap.add_argument("--steps-per-call", type=int, default=0,
                     help="rollout mode: env steps per rollout_sampled call (0 = all timed steps in one call)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the cores this process "
@@ -313,16 +315,21 @@ def main(argv=None):
     per_env = algorithmic_bytes_per_env_step(env)
     achieved = per_env * E / (kern_ms * 1e-3) / 1e9
     metric_cfg = args.config == CONFIG and not args.agents and not args.n_data_msg
-    prof = _profile("r02_kernel_profile.json") if metric_cfg and args.mode == "rollout" else None
+    prof = _profile(PROFILE) if metric_cfg and args.mode == "rollout" else None
+    if prof and prof.get("slices", 2) != args.slices:  # measured on another launch shape
+        prof = None
+    kernel = "k_env_rollout" if args.mode == "rollout" and args.slices == 0 else "k_env_step"
     traffic = round(prof["hbm_bytes_per_env_step"] * E) if prof and prof.get("hbm_bytes_per_env_step") else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
-                "kernel": "k_env_step", "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env,
-                "units_per_launch": E, "launches_per_step": args.slices if args.mode == "rollout" else 3}
+                "kernel": kernel, "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env,
+                "units_per_launch": E,
+                "launches_per_step": (args.slices or round(1 / T, 6)) if args.mode == "rollout" else 3}
     issue = None
     if prof:
-        roofline["rocprof"] = {k: prof[k] for k in ("kernel_avg_us", "launches", "envs_per_launch",
-                                                    "launches_in_flight", "source") if k in prof}
+        roofline["rocprof"] = {k: prof[k] for k in ("kernel_avg_us", "launches", "steps_per_launch",
+                                                    "kernel_us_per_step", "envs_per_launch", "launches_in_flight",
+                                                    "source") if k in prof}
         if prof.get("salu_per_env_step"):
             # the CU's one scalar ALU, shared by its waves, is the scarcest pipe
             a = prof["salu_per_env_step"] * world * E * args.steps / elapsed / N_CU / world
@@ -349,7 +356,9 @@ def main(argv=None):
         "data": f"synthetic LOBSTER day ({args.n_msgs} msgs, PCG64 seed 20260403, mid {args.mid})",
         "config": {"workload": workload, "num_envs_per_gpu": E, "num_envs_total": world * E,
                    "parallelism": f"dp{world} (env shards of one {world * E}-env Speed_test rollout)",
-                   "launch": (f"{args.slices} env slices on their own streams, {T} steps per rollout_sampled call"
+                   "launch": ((f"one persistent k_env_rollout launch of {T} steps per rollout_sampled call "
+                               "(every env's steps back to back, its book kept in LDS)" if args.slices == 0 else
+                               f"{args.slices} env slices on their own streams, {T} steps per rollout_sampled call")
                               if args.mode == "rollout" else "split_keys + sample_actions + env.step per step"),
                    "mode": args.mode, "seeds": "Speed_test: split(PRNGKey(0), NUM_ENVS + 1)"},
         "roofline": roofline,

@@ -403,10 +403,11 @@ template <int S> DEV void fetch_side(SideRows<S>& f, const i32* g, const Valid<S
         }
     }
 }
-// fetched rows -> LDS side table; returns the side's CLEAN / NEG1 bits.  The
-// per-row "any field == -1" / "all fields == -1" tests run as unsigned min /
-// max of the complemented fields (VALU), not as chains of lane-mask logic.
-template <bool ASKS, int S> DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) {
+// fetched rows -> LDS side table (WRITE; else the rows are the table's own); returns the side's
+// CLEAN / NEG1 bits.  The per-row "any field == -1" / "all fields == -1" tests run as unsigned
+// min / max of the complemented fields (VALU), not as chains of lane-mask logic.
+template <bool ASKS, int S>
+DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) {
     const int l = lane_id();
     lmask bad = 0, n1 = 0, pm1 = 0;
 #pragma unroll
@@ -429,6 +430,15 @@ template <bool ASKS, int S> DEV u32 commit_side(Side<S>& s, const SideRows<S>& f
     s.top = -1;
     return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u) |
            (pm1 != 0ull ? SideBits<ASKS>::PM1 : 0u);
+}
+// a side whose table is already in LDS (k_env_rollout: the wave's previous step left it there,
+// and its flags): the register price column from the table
+template <int S> DEV void relink_side(Side<S>& s, int R, const Valid<S>& V) {
+    i32 p[S];
+    ldcol(s.t, R, FP, p);
+#pragma unroll
+    for (int r = 0; r < S; ++r) s.pc[r] = V.v[r] ? p[r] : -1;
+    s.top = -1;
 }
 template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
     SideRows<S> f;
@@ -2264,13 +2274,13 @@ template <int S, int NFIX, bool RC>
 // reference, not a pointer: an address-taken local would live in scratch memory.)
 // key_n / ek: the env count of the step-key split and this env's index in it;
 // e: this env's record / output index
-DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u32* __restrict__ keys, bool master,
+DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u32* __restrict__ keys, bool master,
                       Key& mk,
                       i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
                       const i32* __restrict__ init_states, i32* __restrict__ state, float* __restrict__ obs_out,
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
                       i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
-                      i32* lds) {
+                      i32* lds, bool resident, bool keep, u32& fl_carry) {
     STAMP(t_start);
 #ifdef HFTLOB_STAMPS
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the in-kernel clock
@@ -2287,8 +2297,10 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const int R = B.c.nO;
     book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
     SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
-    fetch_side(fa, rec + c.off_asks, B.vs);
-    fetch_side(fb, rec + c.off_bids, B.vs);
+    if (!resident) {
+        fetch_side(fa, rec + c.off_asks, B.vs);
+        fetch_side(fb, rec + c.off_bids, B.vs);
+    }
     // the agent states (<= 64 words: one per lane), loaded with the book: the agent and reward
     // phases read them with v_readlane instead of waiting on scalar loads per agent
     const int naw = c.rec_words - c.off_agents;
@@ -2336,8 +2348,14 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         py = reinterpret_cast<const int4*>(g)[1];
         if (ftime) fixed_time_mask(px, py, t_end);
     }
-    B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs);
-    B.fl |= fast_bit(B.fl);
+    if (resident) {  // the book flags as the previous step left them (the cached best quotes are not kept)
+        relink_side(B.a, R, B.vs);
+        relink_side(B.b, R, B.vs);
+        B.fl = fl_carry & ~(u32)(F_OK_A | F_OK_B);
+    } else {
+        B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs);
+        B.fl |= fast_bit(B.fl);
+    }
     STAMP(t_load);
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
@@ -2548,11 +2566,15 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     WorldView wv;
     wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
     wv.vol_a = side_volume(B.a, R, B.vs); wv.vol_b = side_volume(B.b, R, B.vs);
-    // the book is final: store it now (frees its registers for the rewards);
-    // an auto-reset below overwrites the record anyway
-    store_side(B.a, rec + c.off_asks, R, B.vs);
-    store_side(B.b, rec + c.off_bids, R, B.vs);
-    store_trades(B.tr, rec + c.off_trades, B.vt);
+    // the book is final: store it now (frees its registers for the rewards).  Not when the
+    // auto-reset below rewrites the record anyway, nor while the wave's next step (keep,
+    // k_env_rollout) takes the book and trade log from LDS as they are
+    if (keep) fl_carry = B.fl;
+    if (!all & !keep) {
+        store_side(B.a, rec + c.off_asks, R, B.vs);
+        store_side(B.b, rec + c.off_bids, R, B.vs);
+        store_trades(B.tr, rec + c.off_trades, B.vt);
+    }
     wv.step = wadd(step, 1); wv.max_steps = max_steps; wv.mid = X.last_mid;
     wv.t0 = last_t0; wv.t1 = last_t1; wv.it0 = ld_t0; wv.it1 = Lr[LD_T1];
     const float dt = i2f(last_t0) + i2f(last_t1) / 1e9f - i2f(wt0) - i2f(wt1) / 1e9f;  // marl_env.py:496
@@ -2666,13 +2688,14 @@ DEV void env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
         env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt,
                          ftime);
-        return;
+        return true;
     }
     if (l == 0) {
         rec[c.off_loaded + LD_STEP] = wadd(step, 1);
         i32* W = rec + c.off_world;
         W[W_T0] = last_t0; W[W_T1] = last_t1; W[W_OIDC] = wsub(oidc, A); W[W_MID] = fbit(new_mid); W[W_DT] = fbit(dt);
     }
+    return false;
 }
 
 // One launch = one batched step.  Env slices: block e steps record e of the
@@ -2691,9 +2714,10 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
     if (e >= n_env) return;
     Key mk{0u, 0u};
     if (master) mk = Key{master[0], master[1]};
+    u32 fl = 0;
     env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master != nullptr, mk, actions_io, msg_data, init_states,
                               state, out.obs, out.rewards, out.done_all, out.dones, out.info, out.obs_raw, out.msgs,
-                              lds);
+                              lds, false, false, fl);
     if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
 
@@ -2721,6 +2745,12 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
     Key mk{master[0], master[1]};
     // `c` is the first kernel argument: offset 0 of the kernarg segment (constant address space)
     kcfg_t* kp = (kcfg_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    // the book stays in LDS from one step to the next (stored to the record only by the last
+    // step); an auto-reset rewrites the record, and the step after it loads the book from there.
+    // (The 100/100 instantiation only: in the general-size ones the AMDGPU backend moved the
+    // lane masks of the resident branch to VGPRs, which s_ff1's SGPR operand cannot take.)
+    bool resident = false;
+    u32 fl = 0;
 #pragma unroll 1
     for (int t = 0; t < n_steps; ++t) {
         const size_t o = per_step ? (size_t)t * n_env : 0;
@@ -2730,13 +2760,13 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         const i32* is = init_states;
         asm volatile("" : "+s"(cp), "+s"(st), "+s"(md), "+s"(is));
         const hftlob_env_cfg& cc = *(const hftlob_env_cfg*)cp;
-        env_step_dev<S, NFIX, RC>(cc, key_n, key_e0 + e, e, nullptr, true, mk,
-                                  actions_io ? actions_io + o * cc.action_words : nullptr, md, is, st,
-                                  out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents,
-                                  out.done_all + o, out.dones + o * cc.n_agents,
-                                  out.info ? out.info + o * cc.info_words : nullptr,
-                                  out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
-                                  out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr, lds);
+        const bool reset = env_step_dev<S, NFIX, RC>(
+            cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
+            is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
+            out.dones + o * cc.n_agents, out.info ? out.info + o * cc.info_words : nullptr,
+            out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
+            out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr, lds, NFIX > 0 && resident, NFIX > 0 && t + 1 < n_steps, fl);
+        resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
     }
     if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }

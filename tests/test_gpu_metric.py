@@ -2,8 +2,8 @@
 2_player_fq_fqc.json, NUM_ENVS = 4096, the 400k-message synthetic day (mid 2 M and 28 M: the
 GOOG-like regime rounds prices above 2^24 in float32), Speed_test's seeds
 (master_key, *reset_keys = split(PRNGKey(0), NUM_ENVS + 1), Speed_test.py:147) and its rollout
-(Speed_test.py:186-196) as the bench runs it: MARLEnv.rollout_sampled over 2 env slices on their
-own streams, 66 steps (the 64-step episode's auto-reset included).  The end state (every integer
+(Speed_test.py:186-196) as the bench runs it: MARLEnv.rollout_sampled as one persistent launch or
+over 2 env slices on their own streams, 66 steps (the 64-step episode's auto-reset included).  The end state (every integer
 word bit-exact, float words within 1e-5) and the carried master key must equal the CPU oracle's
 rollout of the same workload.  Also: a rank's shard of a rollout (key_e0 / key_n, bench.py
 --gpus N) equals its rows of the whole-batch rollout."""
@@ -28,8 +28,11 @@ def _metric_day(mid):
     return _METRIC_DAYS[mid]
 
 
-@pytest.mark.parametrize("mid", [2_000_000, 28_000_000])
-def test_metric_shape_rollout_parity(mid):
+@pytest.mark.parametrize("mid,G", [(2_000_000, 2), (28_000_000, 2), (2_000_000, 0), (28_000_000, 0)])
+def test_metric_shape_rollout_parity(mid, G):
+    """G env slices on their own streams, or G = 0: one persistent k_env_rollout launch whose waves
+    keep their book in LDS from step to step (the book is stored to the record by the last step
+    and reloaded after an auto-reset)."""
     cfg = builtin_config("2_player_fq_fqc")
     day = _metric_day(mid)
     env = MARLEnv(None, cfg, data=day, return_info=False, persistent_outputs=True)
@@ -44,7 +47,7 @@ def test_metric_shape_rollout_parity(mid):
     o_state, _ = O.env_reset(env.cfg_c, o_keys[1:], init)
     _compare_state(env, o_state, state.buf.cpu().numpy(), "reset")
     kin, kout = all_keys[0].clone(), torch.empty(2, dtype=torch.int32, device="cuda")
-    env.rollout_sampled(kin, kout, state, params, T, n_slices=2)       # the bench's launch path
+    env.rollout_sampled(kin, kout, state, params, T, n_slices=G)       # the bench's launch paths
     torch.cuda.synchronize()
     o_end, o_master = O.rollout_sampled(env.cfg_c, o_keys[0], day.msgs, init, o_state, T)
     _compare_state(env, o_end, state.buf.cpu().numpy(), f"after {T} steps")

@@ -1,8 +1,13 @@
 """Summarise a tools/profile_round.sh directory: kernel stats, HBM traffic per
-k_env_step launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), SQ counters
-per wave.  Writes <dir>/pmc_traffic.json and <dir>/kernel_profile.json (what bench.py
-reads from profiles/rNN_kernel_profile.json for the roofline's traffic and the issue
-roofline) and prints a text summary."""
+env-step (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), SQ counters per env-step.
+Writes <dir>/pmc_traffic.json and <dir>/kernel_profile.json (what bench.py reads from
+profiles/rNN_kernel_profile.json for the roofline's traffic and the issue roofline) and
+prints a text summary.
+
+The metric kernel is k_env_step (env slices: one launch = one step of E / G envs, G launches
+in flight) or k_env_rollout (the persistent launch: every wave runs its env's steps back to
+back; per-wave counters are divided by the steps per launch, `steps_per_launch` in
+<dir>/shape.json, written by profile_round.sh)."""
 import csv
 import glob
 import json
@@ -17,7 +22,13 @@ def rows(sub, pat="*counter_collection.csv"):
     return list(csv.DictReader(open(f[0]))) if f else []
 
 
-def per_launch(sub, counter, kernel="k_env_step"):
+shape = json.load(open(os.path.join(d, "shape.json"))) if os.path.exists(os.path.join(d, "shape.json")) else {}
+KERNEL = shape.get("kernel", "k_env_step")
+SPL = shape.get("steps_per_launch", 1)        # PMC passes: env-steps per wave per launch
+STATS_SPL = shape.get("stats_steps_per_launch", 1)  # the stats run: steps per launch
+
+
+def per_launch(sub, counter, kernel=KERNEL):
     vals = [float(r["Counter_Value"]) for r in rows(sub) if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return sum(vals) / len(vals) if vals else None
 
@@ -29,49 +40,52 @@ if stats:
     for r in csv.DictReader(open(stats[0])):
         print(f"{r['Name'][:60]:60s} calls {r['Calls']:>6s} avg_ns {float(r['AverageNs']):12.1f} "
               f"total_pct {float(r['Percentage']):6.2f}")
-        if "k_env_step" in r["Name"] and kstat is None:
+        if KERNEL in r["Name"] and kstat is None:
             kstat = {"kernel_avg_us": round(float(r["AverageNs"]) / 1e3, 2), "launches": int(r["Calls"]),
-                     "kernel_name": r["Name"]}
+                     "kernel_name": r["Name"], "steps_per_launch": STATS_SPL,
+                     "kernel_us_per_step": round(float(r["AverageNs"]) / 1e3 / STATS_SPL, 3)}
 fetch_kb, write_kb = per_launch("fetch", "FETCH_SIZE"), per_launch("write", "WRITE_SIZE")
 bench = json.load(open(os.path.join(d, "stats_bench.json"))) if os.path.exists(os.path.join(d, "stats_bench.json")) else {}
 E = bench.get("config", {}).get("num_envs_per_gpu", 4096)
-G = bench.get("roofline", {}).get("launches_per_step", bench.get("roofline", {}).get("slices", 1))
-# env slices: one k_env_step launch steps E / G envs
+G = shape.get("slices", bench.get("roofline", {}).get("launches_per_step", 1)) or 1
+# env slices: one k_env_step launch steps E / G envs; the persistent launch steps all E envs SPL times
 out = {}
 if fetch_kb is not None and write_kb is not None:
     hbm = (2 * fetch_kb + write_kb) * 1024
-    out = {"kernel": "k_env_step", "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
+    out = {"kernel": KERNEL, "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section)",
-           "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_env_step": round(hbm * G / E, 1),
-           "envs_per_launch": E // G}
+           "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_env_step": round(hbm * G / E / SPL, 1),
+           "envs_per_launch": E // G, "steps_per_launch": SPL}
     json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
-    print("== HBM traffic per k_env_step launch:", json.dumps(out))
+    print(f"== HBM traffic per {KERNEL} launch:", json.dumps(out))
 sq = {}
 for r in rows("sq"):
-    if "k_env_step" in r["Kernel_Name"]:
+    if KERNEL in r["Kernel_Name"]:
         sq.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 per_wave = {}
 if sq:
     w = sum(sq["SQ_WAVES"]) / len(sq["SQ_WAVES"])
-    per_wave = {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(sq.items()) if k != "SQ_WAVES"}
-    print("== SQ counters per wave (k_env_step):", per_wave)
+    per_wave = {k.replace("SQ_", ""): round(sum(v) / len(v) / w / SPL, 1) for k, v in sorted(sq.items())
+                if k != "SQ_WAVES"}
+    print(f"== SQ counters per wave and env-step ({KERNEL}):", per_wave)
 lds = {}
 for r in rows("lds"):
-    if "k_env_step" in r["Kernel_Name"]:
+    if KERNEL in r["Kernel_Name"]:
         lds.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 if lds:
     w = sum(lds["SQ_WAVES"]) / len(lds["SQ_WAVES"])
-    print("== SQ LDS / issue counters per wave (k_env_step):",
-          {k.replace("SQ_", ""): round(sum(v) / len(v) / w, 1) for k, v in sorted(lds.items()) if k != "SQ_WAVES"})
+    print(f"== SQ LDS / issue counters per wave and env-step ({KERNEL}):",
+          {k.replace("SQ_", ""): round(sum(v) / len(v) / w / SPL, 1) for k, v in sorted(lds.items()) if k != "SQ_WAVES"})
 sm = os.path.join(d, "bench_stepmode.json")
 if os.path.exists(sm) and os.path.getsize(sm):
     b = json.load(open(sm))
     print("== step mode (split_keys + sample_actions + env.step, 3 launches):", b["value"], "env steps/s,",
           b["ms_per_step"], "ms/step")
 
-# one wave per env and one env-step per wave per k_env_step launch: per-wave counts are per env-step
+# one wave per env: per-wave counts / steps per launch are per env-step
 prof = dict(kstat or {})
-prof.update({"envs_per_launch": E // G, "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d))})
+prof.update({"kernel": KERNEL, "slices": shape.get("slices", G), "envs_per_launch": E // G,
+             "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d))})
 if "INSTS_SALU" in per_wave:
     prof["salu_per_env_step"] = per_wave["INSTS_SALU"]
     prof["valu_per_env_step"] = per_wave.get("INSTS_VALU")
