@@ -423,10 +423,14 @@ class MARLEnv:
 
     @staticmethod
     def default_slices(n_env: int) -> int:
-        """Env slices for rollout_sampled, measured on 1x MI355X: 2 slices from
-        2048 envs up (4096: +11 %, 8192: +19 %); below that the slices' extra launches cost more
-        than the step tails they hide (512 envs: -6 %)."""
-        return 2 if n_env >= 2048 else 1
+        """Launch shape of rollout_sampled, measured on 1x MI355X (DESIGN.md section 4,
+        tools/sweep_envs.sh): 0 = one persistent launch (every env's steps back to back, its book
+        kept in LDS) while the whole batch is resident (16 envs per CU: up to 4096 envs;
+        512 / 2048 / 4096 envs: 9.9 / 33.5 / 49.6 M env-steps/s against 7.7 / 28.3 / 47.5 M for
+        2 slices); above that 2 env slices on their own streams (8192 / 16384 envs: 57.2 / 58.9 M
+        against 53.0 / 56.5 M persistent, whose second wave of workgroups waits for a whole
+        rollout of the first)."""
+        return 0 if n_env <= 4096 else 2
 
     def prepare_rollout(self, n_slices: int) -> None:
         """Create the library's slice streams for `n_slices` on this env's device (host-only).
