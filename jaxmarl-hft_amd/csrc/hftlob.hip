@@ -994,9 +994,31 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
     ldcol(s.t, R, FOID, o);
     ldcol(s.t, R, FQ, q);
     lmask fm[S];
+    int idx;
+#ifdef HFTLOB_CANCEL_1PASS
+    if (!RC) {  // the id match and the init-id fallback in one pass (no branch between them)
+        const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
+        const u32 span = (u32)wsub(B.c.init_id, lo);
+        lmask ff[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
+            u32 d = vkeep((u32)wsub(o[r], lo));
+            d = vkeep(s.pc[r] == m.price ? d : 0xFFFFFFFFu);
+            d = vkeep(q[r] >= m.qty ? d : 0xFFFFFFFFu);
+            ff[r] = B.vs.m[r] & bal(d <= span);
+        }
+        u32 a = ff1(fm[0]), b = ff1(ff[0]);
+#pragma unroll
+        for (int r = 1; r < S; ++r) { a = min(a, ff1(fm[r]) | (u32)(64 * r)); b = min(b, ff1(ff[r]) | (u32)(64 * r)); }
+        b = b == 0xFFFFFFFFu ? (u32)(R - 1) : b;
+        idx = (int)(a == 0xFFFFFFFFu ? b : a);
+    } else
+#endif
+    {
 #pragma unroll
     for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
-    int idx = first_slot(fm, -1);
+    idx = first_slot(fm, -1);
     if (idx < 0) {
         // get_init_id_match: price == msg price, init_id - 2 * depth <= oid <= init_id, q >= msg q.
         // Evaluated per lane in VALU (selects feeding one compare), not as three lane masks ANDed on
@@ -1028,6 +1050,7 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
             }
             if (idx < 0) idx = R - 1;
         }
+    }
     }
     const i32 op = sget(s.pc, idx), oq = sget(q, idx);
     // FAST sides: a p == -1 row holds -1 in every field but q (a cancel of a negative quantity can
