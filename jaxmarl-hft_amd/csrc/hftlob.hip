@@ -403,9 +403,9 @@ template <int S> DEV void fetch_side(SideRows<S>& f, const i32* g, const Valid<S
         }
     }
 }
-// fetched rows -> LDS side table (WRITE; else the rows are the table's own); returns the side's
-// CLEAN / NEG1 bits.  The per-row "any field == -1" / "all fields == -1" tests run as unsigned
-// min / max of the complemented fields (VALU), not as chains of lane-mask logic.
+// fetched rows -> LDS side table; returns the side's CLEAN / NEG1 bits.  The per-row "any field
+// == -1" / "all fields == -1" tests run as unsigned min / max of the complemented fields (VALU),
+// not as chains of lane-mask logic.
 template <bool ASKS, int S>
 DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) {
     const int l = lane_id();
@@ -994,31 +994,9 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
     ldcol(s.t, R, FOID, o);
     ldcol(s.t, R, FQ, q);
     lmask fm[S];
-    int idx;
-#ifdef HFTLOB_CANCEL_1PASS
-    if (!RC) {  // the id match and the init-id fallback in one pass (no branch between them)
-        const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
-        const u32 span = (u32)wsub(B.c.init_id, lo);
-        lmask ff[S];
-#pragma unroll
-        for (int r = 0; r < S; ++r) {
-            fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
-            u32 d = vkeep((u32)wsub(o[r], lo));
-            d = vkeep(s.pc[r] == m.price ? d : 0xFFFFFFFFu);
-            d = vkeep(q[r] >= m.qty ? d : 0xFFFFFFFFu);
-            ff[r] = B.vs.m[r] & bal(d <= span);
-        }
-        u32 a = ff1(fm[0]), b = ff1(ff[0]);
-#pragma unroll
-        for (int r = 1; r < S; ++r) { a = min(a, ff1(fm[r]) | (u32)(64 * r)); b = min(b, ff1(ff[r]) | (u32)(64 * r)); }
-        b = b == 0xFFFFFFFFu ? (u32)(R - 1) : b;
-        idx = (int)(a == 0xFFFFFFFFu ? b : a);
-    } else
-#endif
-    {
 #pragma unroll
     for (int r = 0; r < S; ++r) fm[r] = B.vs.m[r] & bal(o[r] == m.oid);
-    idx = first_slot(fm, -1);
+    int idx = first_slot(fm, -1);
     if (idx < 0) {
         // get_init_id_match: price == msg price, init_id - 2 * depth <= oid <= init_id, q >= msg q.
         // Evaluated per lane in VALU (selects feeding one compare), not as three lane masks ANDed on
@@ -1050,7 +1028,6 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
             }
             if (idx < 0) idx = R - 1;
         }
-    }
     }
     const i32 op = sget(s.pc, idx), oq = sget(q, idx);
     // FAST sides: a p == -1 row holds -1 in every field but q (a cancel of a negative quantity can
