@@ -256,7 +256,7 @@ def main(argv=None):
     state0 = state.buf.clone()
     key_e0, key_n = rank * E, world * E
     if args.slices < 0:
-        args.slices = MARLEnv.default_slices(E)
+        args.slices = env.default_slices(E)
     if args.mode == "rollout":
         env.prepare_rollout(args.slices)
     T = (args.steps_per_call if args.steps_per_call > 0 else max(args.steps, 1)) if args.mode == "rollout" else 1

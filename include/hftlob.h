@@ -289,7 +289,8 @@ int hftlob_env_step_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, con
  * passes its offset, so N ranks together replay the single-device rollout.
  * n_slices = 0: ONE kernel launch for all n_steps; every env (one wavefront)
  * runs its steps back to back with its own copy of the master-key chain, so no
- * step boundary waits for the batch's slowest env.
+ * step boundary waits for the batch's slowest env (for 100/100-slot books the
+ * book also stays in LDS between steps; the last step stores it to `state`).
  * n_slices = 1..4: the envs are cut into n_slices contiguous slices, each stepped
  * by one launch per step: slice 0 on `stream`, the others on library-owned HIP
  * streams of the stream's device, forked from / joined back to it with events

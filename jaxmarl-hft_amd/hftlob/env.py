@@ -421,16 +421,33 @@ class MARLEnv:
                   _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf), C.byref(o["struct"]))
         return self._results(o, state, E)
 
-    @staticmethod
-    def default_slices(n_env: int) -> int:
+    LDS_PER_CU = 160 * 1024      # MI355X (gfx950) LDS per CU
+    ROLLOUT_WAVES_PER_CU = 16    # k_env_rollout: launch_bounds(64, 4), ~105 VGPRs -> 4 waves per SIMD
+
+    def lds_bytes_per_env(self) -> int:
+        """Dynamic LDS of one env's workgroup (env_shm in hftlob.hip): agent rows, action extras,
+        the two book sides, the trade log and the scratch row."""
+        c = self.cfg_c
+        return 4 * ((c.n_cancel_msgs + c.n_action_msgs) * 8 + ((c.n_agents * 6 + 3) & ~3) +
+                    12 * c.lob.n_orders + 8 * c.lob.n_trades + 64 * 4)
+
+    def resident_envs(self) -> int:
+        """Envs of this config the GPU holds at once (workgroups per CU by LDS and by waves)."""
+        per_cu = min(self.ROLLOUT_WAVES_PER_CU, self.LDS_PER_CU // self.lds_bytes_per_env())
+        n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count \
+            if torch.cuda.is_available() else 256
+        return per_cu * n_cu
+
+    def default_slices(self, n_env: int) -> int:
         """Launch shape of rollout_sampled, measured on 1x MI355X (DESIGN.md section 4,
-        tools/sweep_envs.sh): 0 = one persistent launch (every env's steps back to back, its book
-        kept in LDS) while the whole batch is resident (16 envs per CU: up to 4096 envs;
-        512 / 2048 / 4096 envs: 9.9 / 33.5 / 49.6 M env-steps/s against 7.7 / 28.3 / 47.5 M for
-        2 slices); above that 2 env slices on their own streams (8192 / 16384 envs: 57.2 / 58.9 M
-        against 53.0 / 56.5 M persistent, whose second wave of workgroups waits for a whole
-        rollout of the first)."""
-        return 0 if n_env <= 4096 else 2
+        tools/sweep_envs.sh, tools/gpu_sweep.sh): 0 = one persistent launch (every env's steps back
+        to back, its book kept in LDS) while the whole batch is resident (the metric config: 16
+        envs per CU, 4096 envs; 512 / 2048 / 4096 envs: 9.9 / 33.5 / 49.6 M env-steps/s against
+        7.7 / 28.3 / 47.5 M for 2 slices); otherwise 2 env slices on their own streams (8192 /
+        16384 envs: 57.2 / 58.9 M against 53.0 / 56.5 M persistent, whose later workgroups wait for
+        whole rollouts of the first; Speed_test's [5,5] / [10,10] agents at 4000 envs, whose agent
+        rows leave room for 14 / 11 envs per CU: 24.1 / 14.7 M against 19.4 / 11.4 M)."""
+        return 0 if n_env <= self.resident_envs() else 2
 
     def prepare_rollout(self, n_slices: int) -> None:
         """Create the library's slice streams for `n_slices` on this env's device (host-only).

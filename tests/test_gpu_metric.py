@@ -7,6 +7,8 @@ over 2 env slices on their own streams, 66 steps (the 64-step episode's auto-res
 word bit-exact, float words within 1e-5) and the carried master key must equal the CPU oracle's
 rollout of the same workload.  Also: a rank's shard of a rollout (key_e0 / key_n, bench.py
 --gpus N) equals its rows of the whole-batch rollout."""
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -73,3 +75,17 @@ def test_rollout_shards_equal_whole_batch():
         env.rollout_sampled(keys[0].clone(), ko, s, params, T, n_slices=1 + r % 2, key_e0=r * E, key_n=N * E)
         assert (ko == kout).all(), f"rank {r}: carried key"
         assert (s.buf == whole.buf[r * E:(r + 1) * E]).all(), f"rank {r}: state"
+
+
+def test_default_launch_shape():
+    """MARLEnv.default_slices: the persistent launch while the whole batch is resident (the
+    metric: 4096 envs at 16 per CU), 2 env slices beyond, and for configs whose agent rows leave
+    fewer envs per CU (Speed_test's [5, 5] agents at 4000 envs; profiles/r02_*sweep*)."""
+    cfg = builtin_config("2_player_fq_fqc")
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
+    assert env.lds_bytes_per_env() * 16 <= env.LDS_PER_CU
+    assert env.default_slices(4096) == 0 and env.default_slices(512) == 0
+    assert env.default_slices(8192) == 2
+    big = dataclasses.replace(builtin_config("default"), number_of_agents_per_type=[5, 5])
+    env5 = MARLEnv(None, big, data=_day(big.world_config, 2_000_000))
+    assert env5.default_slices(4000) == 2

@@ -11,7 +11,7 @@ T=${1:-r01}
 O=$GRAFT_REPO_ROOT/gpurun_out/prof_$T
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
-G=${SLICES:-$(python -c "import sys; sys.path.insert(0, 'jaxmarl-hft_amd'); from hftlob.env import MARLEnv; print(MARLEnv.default_slices(4096))")}
+G=${SLICES:-0}  # the metric's default shape (MARLEnv.default_slices: the persistent launch at 4096 envs)
 if [ "$G" = 0 ]; then
   KER=k_env_rollout; STATS_ARGS="--warmup 128 --steps 128"; PMC_ARGS="--warmup 0 --steps 32"; SPL=32; SSPL=128
 else
