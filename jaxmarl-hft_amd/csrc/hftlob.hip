@@ -344,11 +344,6 @@ struct Side {
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid under F_OK
     i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
                          // every handler reads prices, only adds and row clears write them
-    // top-of-book cache: the slot _get_top_*_order_idx returns for max / min price top_p, and its
-    // (ts, tns); top = -1: unknown.  Kept across messages: a quantity change keeps it, clearing the
-    // row (or any bulk clear) drops it, an add at a better price or an earlier time at top_p
-    // replaces it (see top_new / top_eq), so a crossing message usually skips the top-of-book scan
-    i32 top, top_p, top_ts, top_tns;
 };
 
 // slot e of a lane-strided register column <- v (lane e & 63 of register e >> 6): one
@@ -427,7 +422,6 @@ DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) 
         pm1 |= V.m[r] & bal((p == -1) & (all0 != 0u));
     }
     lds_order();
-    s.top = -1;
     return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u) |
            (pm1 != 0ull ? SideBits<ASKS>::PM1 : 0u);
 }
@@ -438,7 +432,6 @@ template <int S> DEV void relink_side(Side<S>& s, int R, const Valid<S>& V) {
     ldcol(s.t, R, FP, p);
 #pragma unroll
     for (int r = 0; r < S; ++r) s.pc[r] = V.v[r] ? p[r] : -1;
-    s.top = -1;
 }
 template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
     SideRows<S> f;
@@ -472,7 +465,6 @@ template <int S> DEV void clear_masked(Side<S>& s, int R, const lmask (&m)[S]) {
         }
     }
     lds_order();
-    s.top = -1;
 }
 
 // _removeZeroNegQuant — JaxOrderBookArrays.py:85-90 on a side that is not
@@ -635,62 +627,35 @@ struct Msg {
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
 // side: it changes (best_p, best_q) only where get_best_* / get_volume_at_price
 // would, and falls back to a full recompute (ok = false) where it cannot tell.
-// the top-of-book cache after an order (np, t, tns) went to slot e:
-// a new best price: the row is alone at it, so it is the top (unless a maxint time, where the
-// top-of-book formula's maxint placeholders could tie with it)
-template <int S> DEV void top_new(Side<S>& s, int e, i32 np, i32 t, i32 tns, i32 maxint) {
-    s.top = ((t != maxint) & (tns != maxint)) ? e : -1;
-    s.top_p = np; s.top_ts = t; s.top_tns = tns;
-}
-// an order at the best price: the top moves to it only if it is earlier in (ts, tns, slot)
-// (a known top is at the best price, np: note_add drops it whenever the best quote is not known;
-// one branch per test, the common case first: an OR of the tests becomes 64-bit lane-mask logic
-// on the scalar unit)
-template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) {
-    if (fresh(t) > s.top_ts) return;  // a later order (the common case)
-    asm volatile("");
-    if (s.top < 0) return;
-    asm volatile("");
-    bool earlier = t < s.top_ts;
-    if (!earlier) earlier = (tns < s.top_tns) | ((tns == s.top_tns) & (e < s.top));
-    if (earlier) {
-        s.top = tns != maxint ? e : -1;  // (t < top_ts < maxint)
-        s.top_ts = t; s.top_tns = tns;
-    }
-}
-template <bool BID, int S>
-DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint) {
-    // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
-    // common case, an order behind the best (one compare each); per side the cases are those of
-    // get_best_* with -1 (and, for asks, maxint) standing for "no price".
+template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq, i32 maxint) {
+    // an all -1 row now holds (np, nq > 0).  Branches ordered for the common case, an order
+    // behind the best (one compare each); per side the cases are those of get_best_* with -1
+    // (and, for asks, maxint) standing for "no price".
     constexpr u32 OK = SideBits<!BID>::OK;
-    if (!(fl & OK)) { s.top = -1; return; }
+    if (!(fl & OK)) return;
     const i32 bp = s.best_p;
     if (BID) {
         if (np < bp) {
             if (bp == -1) fl &= ~OK;        // np < -1 on an empty side
         } else if (np > bp) {
             s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
-            top_new(s, e, np, t, tns, maxint);
         } else if (bp == -1) {
             fl &= ~OK;                      // np == -1 on an empty side
         } else {
             s.best_q = wadd(s.best_q, nq);
-            top_eq(s, e, t, tns, maxint);
         }
     } else {
         if (np > bp) {
             if (bp == -1) {                 // empty side
                 if (np == maxint) fl &= ~OK;
-                else { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
+                else { s.best_p = np; s.best_q = nq; }
             }
         } else if (np < bp) {
-            if (np != -1) { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
+            if (np != -1) { s.best_p = np; s.best_q = nq; }
         } else if (np == -1) {
             fl &= ~OK;
         } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
-            top_eq(s, e, t, tns, maxint);
         }
     }
 }
@@ -724,7 +689,6 @@ template <int S> DEV void side_put(Side<S>& s, int R, int e, i32 f0, i32 f1, i32
 template <int S> DEV void side_clr(Side<S>& s, int R, int e) {
     clr6(s.t, s.scr, R, e);
     col_set(s.pc, e, -1);
-    s.top = e == s.top ? -1 : s.top;
 }
 // the side's p == -1 slots (all -1 rows in the FAST variant)
 template <int S> DEV void free_slots(const Book<S>& B, const Side<S>& s, lmask (&free)[S]) {
@@ -802,21 +766,11 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
         } else if (mp < price) {
             break;
         }
-        int top;
-        i32 qt, ot, tt;
-        if (s.top >= 0 && s.top_p == mp) {  // the cached top: three broadcast reads
-            top = s.top;
-            qt = ldu(s.t, R, FQ, top); ot = ldu(s.t, R, FOID, top); tt = ldu(s.t, R, FTID, top);
-        } else {
-            i32 q[S], o[S], t[S], ts[S], tn[S];
-            ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
-            ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
-            top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
-            qt = sget(q, top); ot = sget(o, top); tt = sget(t, top);
-            const i32 tts = sget(ts, top), ttn = sget(tn, top);
-            s.top_p = mp; s.top_ts = tts; s.top_tns = ttn;
-            s.top = ((mp != -1) & (mp != B.c.maxint) & (tts != B.c.maxint) & (ttn != B.c.maxint)) ? top : -1;
-        }
+        i32 q[S], o[S], t[S], ts[S], tn[S];
+        ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
+        ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
+        const int top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
+        const i32 qt = sget(q, top), ot = sget(o, top), tt = sget(t, top);
         const i32 tp = sget(s.pc, top);
         if (fresh(tp) == -1) break;  // (two branches, not a 64-bit lane-mask OR)
         asm volatile("");
@@ -840,8 +794,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         if (nq > 0) {
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
             if (m.h & (H_NEG1 | H_PM1)) B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
-            if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
-            else { B.fl &= ~OK; s.top = -1; }
+            if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
+            else B.fl &= ~OK;
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
             side_clr(s, R, e);
             B.fl &= ~OK;
@@ -876,8 +830,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         if (m.h & H_NEG1) B.fl |= NEG1;
         if (m.h & H_PM1) B.fl |= PM1;
-        if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
-        else { B.fl &= ~OK; s.top = -1; }
+        if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
+        else B.fl &= ~OK;
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         side_clr(s, R, e);
         B.fl &= ~OK;
@@ -900,11 +854,9 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
     lmask m[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(s.pc[r] == worst);
-    const i32 top = s.top;
     clear_masked(s, R, m);
-    // only the worst level goes: the best quote and the top of book survive unless the side holds
-    // one price level (worst == best; an ask side whose prices are all maxint has best -1)
-    s.top = worst != s.top_p ? top : -1;
+    // only the worst level goes: the best quote survives unless the side holds one price level
+    // (worst == best; an ask side whose prices are all maxint has best -1)
     if ((worst == s.best_p) | (s.best_p == -1)) B.fl &= ~SideBits<!BID>::OK;
     free_slots(B, s, free);
 }
@@ -925,7 +877,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
     }
-    note_add<BID>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
+    note_add<BID>(s, B.fl, m.price, qty, B.c.maxint);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their

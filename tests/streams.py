@@ -54,3 +54,44 @@ def init_book_messages(n_env, seed, price0=1000, tick=1, depth=10):
             q = int(rng.integers(0, 200)) if rng.random() > 0.1 else 0
             m[e, k] = (1, side, q, price0 - side * lvl * tick + (5 if side == -1 else -5), -2, -2 - k, 34199, 0)
     return m
+
+
+def top_streams(n_env, n_msg, seed, price0=1000, maxint=2**31 - 1):
+    """Streams for the top-of-book slot (_get_top_*_order_idx) and time priority: a narrow
+    price band so most orders join or cross the best level, times drawn from a small set (ties on
+    (ts, tns) and orders EARLIER than the standing top are common, so the slot tie-break and the
+    time-priority replacement both run), partial and full fills, cancels at the best price, and a
+    few maxint times."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.zeros((n_env, n_msg, 8), dtype=np.int32)
+    for e in range(n_env):
+        live = []
+        next_oid = 5000
+        for k in range(n_msg):
+            t = 34200 + int(rng.integers(0, 3))
+            tn = int(rng.integers(0, 4)) * 100
+            if rng.random() < 0.01:
+                t = maxint
+            if rng.random() < 0.01:
+                tn = maxint
+            side = int(rng.choice([-1, 1]))
+            price = price0 + side * int(rng.integers(-2, 3))
+            qty = int(rng.integers(1, 40))
+            tid = int(rng.integers(1, 4))
+            u = rng.random()
+            if u < 0.5:
+                typ, oid = 1, next_oid
+                next_oid += 1
+                live.append((oid, side, price))
+            elif u < 0.7 and live:
+                typ = int(rng.choice([2, 3]))
+                oid, side, price = live[int(rng.integers(0, len(live)))]
+            elif u < 0.9:
+                typ = 4
+                oid = live[int(rng.integers(0, len(live)))][0] if live else 7
+            else:                                   # marketable limit: crosses deep
+                typ, oid = 1, next_oid
+                next_oid += 1
+                price = price0 - side * 5
+            out[e, k] = (typ, side, qty, price, oid, tid, t, tn)
+    return out

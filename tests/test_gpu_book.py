@@ -9,7 +9,7 @@ from hftlob.config import JAXLOB_Configuration
 from hftlob.engine import book_process_, scan_through_entire_array_save_bidask
 from hftlob.layout import pack_lob_cfg
 from oracle import pyoracle as O
-from streams import init_book_messages, random_streams
+from streams import init_book_messages, random_streams, top_streams
 
 pytestmark = pytest.mark.gpu
 
@@ -92,3 +92,20 @@ def test_book_empty_and_max_sizes():
     empty_t = np.full((E, 256, 8), -1, np.int32)
     a0, b0, _, _, _ = O.book_process(pack_lob_cfg(big), init, empty_a, empty_a, empty_t, save_best=False)
     _run(big, random_streams(E, M, seed=77), a0, b0, empty_t)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(nOrders=16, nTrades=8), dict(type_4_interpretation=1)],
+                         ids=["default", "nO16", "t4lim"])
+def test_book_top_of_book_cache(kw):
+    """Crossing-heavy streams with tied and out-of-order times (streams.top_streams): every match
+    trip's top-of-book slot equals the oracle's (this stream caught a top-of-book slot cache that
+    the metric's and the random streams did not)."""
+    cfg = JAXLOB_Configuration(**kw)
+    E, M = 64, 400
+    init = init_book_messages(E, seed=5)
+    empty_a = np.full((E, cfg.nOrders, 6), -1, np.int32)
+    empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
+    a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
+    msgs = top_streams(E, M, seed=11 + cfg.nOrders)
+    _run(cfg, msgs, a0, b0, empty_t)
+    _run(cfg, msgs, empty_a, empty_a, empty_t)
