@@ -10,10 +10,14 @@
   state0 and master_key.
 
 The K timed steps are one MARLEnv.rollout_sampled call (hftlob_env_rollout_sampled,
-Speed_test's whole scan): split + sample + step fused per launch, the envs as 2 contiguous
-slices on their own streams so one slice's slowest envs overlap the other slice's next step
-(bit-exact with K full-batch launches, tests/test_gpu_env.py).  --mode step: Speed_test's three
-calls (split_keys, sample_actions, env.step) as three launches per step.
+Speed_test's whole scan): split + sample + step fused.  While the whole batch is resident on
+the GPU (the metric: 4096 envs, 16 one-wave workgroups per CU) that is ONE persistent
+k_env_rollout launch in which every env runs its K steps back to back with its book kept in
+LDS; larger batches run as 2 contiguous env slices on their own streams, one k_env_step launch
+per slice and step, so one slice's slowest envs overlap the other slice's next step
+(MARLEnv.default_slices; both bit-exact with K full-batch launches, tests/test_gpu_env.py).
+--mode step: Speed_test's three calls (split_keys, sample_actions, env.step) as three launches
+per step.
 
 Multi-GPU (weak scaling, one process per GPU): `--gpus N` launches N ranks itself when it is
 not already running under torchrun; rank r owns envs [r*E, (r+1)*E) of ONE Speed_test rollout
@@ -21,7 +25,9 @@ over N*E envs (reset keys split(PRNGKey(0), N*E+1)[1+r*E : 1+(r+1)*E], step keys
 split(master, N*E+1)[1 + r*E + e]: the reference's pmap layout, ippo_rnn_JAXMARL_pmap.py:292-332).
 Day and init-state table are replicated; no collective on the data path (RCCL only for the
 timing barrier and the max over ranks).  --dry-run stops before the GPU (gloo) and prints the
-rank layout.  Rank 0 prints ONE JSON line.
+rank layout.  --dist-backend gloo --same-device runs the multi-rank body with every rank on
+device 0 (a 1-GPU box rehearsing the N-GPU data path; --dump-state DIR writes each rank's end
+state and carried key for the parity test).  Rank 0 prints ONE JSON line.
 """
 import argparse
 import hashlib
@@ -66,6 +72,12 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the cores this process "
                                                                "may use, capped by OMP_NUM_THREADS)")
     ap.add_argument("--dry-run", action="store_true", help="rank layout only: no GPU (gloo), one JSON line")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process group of the ranks (nccl = RCCL; gloo: the barrier / max on the CPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on device 0 (with --dist-backend gloo: the N-rank body on a 1-GPU box)")
+    ap.add_argument("--dump-state", default=None,
+                    help="directory: each rank writes rank<r>.npz (end state, carried key) after the timed run")
     return ap.parse_args(argv)
 
 
@@ -127,6 +139,38 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def cpu_share():
+    """Host cores this process may use for the CPU baseline: its affinity set, capped by the
+    cgroup CPU quota and by OMP_NUM_THREADS.  The GPU pool runs each 1-GPU job in a share of the
+    host (OMP_NUM_THREADS is set to it there), while nproc / the affinity set show the whole
+    machine: threads beyond the share would only time-slice.  Returns (threads, facts)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path, per in (("/sys/fs/cgroup/cpu.max", None), ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us",
+                                                        "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            with open(path) as f:
+                q = f.read().split()
+            if per is None:
+                if q and q[0] != "max":
+                    quota = int(q[0]) / int(q[1])
+            else:
+                with open(per) as f:
+                    p = int(f.read().split()[0])
+                if int(q[0]) > 0:
+                    quota = int(q[0]) / p
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    omp = os.environ.get("OMP_NUM_THREADS")
+    thr = aff
+    if quota:
+        thr = min(thr, max(1, int(quota)))
+    if omp and omp.isdigit() and int(omp) > 0:
+        thr = min(thr, int(omp))
+    return thr, {"affinity_cores": aff, "cgroup_quota_cores": quota, "omp_num_threads": omp}
+
+
 def _profile(name):
     p = os.path.join(ROOT, "profiles", name)
     if os.path.exists(p):
@@ -181,13 +225,17 @@ def cpu_baseline(env, day, state0, master0, n_threads):
     L.oracle_set_threads(thr)
     if not (st1 == st).all():
         raise AssertionError("cpu_baseline: 1-thread and multi-thread CPU rollouts differ")
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    _, facts = cpu_share()
+    eff = v / (thr * v1) if thr and v1 else None
     return {"value": round(v, 1), "unit": "env steps/s", "cores": thr, "kind": "port",
             "sample": (f"{E} envs x {CPU_STEPS} steps (one episode incl. auto-reset) of the metric config/day/seeds, "
                        "Speed_test rollout loop in C (oracle/oracle.c oracle_rollout_sampled), "
                        f"gcc -O3 -march=native, OpenMP {thr} threads"),
             "single_core_value": round(v1, 1), "single_core_sample": f"the same {E} x {CPU_STEPS} workload, 1 thread",
-            "cpu_model": model, "nproc": os.cpu_count(), "affinity_cores": aff}, st
+            "thread_scaling_efficiency": round(eff, 3) if eff else None,
+            "cores_rule": ("threads = this job's host CPU share: the affinity set capped by the cgroup quota and "
+                           "OMP_NUM_THREADS (bench.py cpu_share)"),
+            "cpu_model": model, "nproc": os.cpu_count(), **facts}, st
 
 
 # ------------------------------------------------------------------ rank body
@@ -217,12 +265,15 @@ def main(argv=None):
     import numpy as np
     import torch
     from hftlob import dist as D
-    R = D.init_from_env("nccl")
-    world, rank, local = R.world, R.rank, R.local
+    if args.same_device and args.dist_backend != "gloo":
+        raise SystemExit("bench: --same-device needs --dist-backend gloo (RCCL takes one GPU per rank)")
+    R = D.init_from_env(args.dist_backend)
+    world, rank, local = R.world, R.rank, (0 if args.same_device else R.local)
     if world != args.gpus:
         print(f"bench: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    red_dev = dev if args.dist_backend == "nccl" else None  # where max_over_ranks reduces
 
     import dataclasses
     from hftlob.config_io import builtin_config
@@ -298,11 +349,15 @@ def main(argv=None):
     D.barrier(R)
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps     # HIP-event time of the timed region per batched step
-    elapsed = D.max_over_ranks(R, elapsed, device=dev)
+    elapsed = D.max_over_ranks(R, elapsed, device=red_dev)
+    if args.dump_state:  # this rank's end state and carried key (tests/test_gpu_bench_ranks.py)
+        os.makedirs(args.dump_state, exist_ok=True)
+        np.savez(os.path.join(args.dump_state, f"rank{rank}.npz"), state=state.buf.cpu().numpy(),
+                 key=kbuf[nstep[0] % 2].cpu().numpy(), key_e0=key_e0, key_n=key_n, steps=args.steps)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        thr = args.cpu_threads or min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "1024")))
+        thr = args.cpu_threads or cpu_share()[0]
         cpu, cpu_state = cpu_baseline(env, day, state0, master0, thr)
         restart()                             # the same rollout on the GPU, for the parity check
         run(CPU_STEPS)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define HFTLOB_ABI_VERSION 6
+#define HFTLOB_ABI_VERSION 7
 
 #define HFTLOB_OK            0
 #define HFTLOB_EINVAL      (-1)   /* bad config value / unsupported option */
@@ -48,6 +48,8 @@ extern "C" {
 #define HFTLOB_MAX_OBS     16     /* observation width upper bound */
 #define HFTLOB_INFO_WORLD_WORDS 14
 #define HFTLOB_INFO_AGENT_WORDS 24
+#define HFTLOB_L2_LEVELS   10     /* get_L2_state levels of world debug_mode (marl_env.py:646-651) */
+#define HFTLOB_DEBUG_WORDS(n_trades) (4 * HFTLOB_L2_LEVELS + 8 * (n_trades))
 
 /* ---- engine configuration: JAXLOB_Configuration (jaxob_config.py:12-30) --- */
 typedef struct hftlob_lob_cfg {
@@ -220,7 +222,16 @@ typedef struct hftlob_env_cfg {
  *            zeroed for done agents and taken before the auto-reset, as info is
  *   msgs     int32 [n_env][n_msgs][8] (step only): the step's combined message
  *            array [cancels; shuffled actions; data] as processed by the book —
- *            the MM "messages" observation (mm_env.py:2820-2821) */
+ *            the MM "messages" observation (mm_env.py:2820-2821), and
+ *            info["world"]["total_msgs"] under world debug_mode
+ *   debug    int32 [n_env][HFTLOB_DEBUG_WORDS(n_trades)] (step only): world
+ *            debug_mode's info (marl_env.py:645-656) of the stepped state, taken
+ *            before the auto-reset as info is: words [0, 40) lob_state =
+ *            get_L2_state(asks, bids, 10) (JaxOrderBookArrays.py:1231-1264: 10 rows
+ *            [ask_p, ask_q, bid_p, bid_q], unique ask prices ascending with -1 read
+ *            as maxint, unique bid prices descending, missing levels maxint /
+ *            -maxint, negative volumes 0), then the step's trade log [n_trades][8]
+ *            (info["world"]["trades"]) */
 typedef struct hftlob_step_out {
     float*   obs;
     float*   rewards;
@@ -229,6 +240,7 @@ typedef struct hftlob_step_out {
     int32_t* info;
     int32_t* obs_raw;
     int32_t* msgs;
+    int32_t* debug;
 } hftlob_step_out;
 
 int         hftlob_version(void);

@@ -712,9 +712,10 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
     const i32 newq = imax_(0, wsub(qt, qtm));
     const i32 rem = wsub(qtm, qt);
     int e;
-    if (B.ntr >= 0) {  // the row after the last written one; a trade with col 4 (aggressor oid) == -1 leaves it free
+    if (B.ntr >= 0) {  // the row after the last written one; a trade whose col 4 (the message time,
+                       // TradesFeat SEC) is -1 leaves its row free for the next trade
         e = imin_(B.ntr, B.c.nT - 1);
-        if (m.oid != -1) B.ntr = imin_(B.ntr + 1, B.c.nT);
+        if (m.t != -1) B.ntr = imin_(B.ntr + 1, B.c.nT);
     } else {
         i32 tr4[S];
         ldcol(B.tr.t, B.tr.R, 4, tr4);
@@ -2232,6 +2233,52 @@ DEV void fixed_time_mask(int4& x, int4& y, i32 t_end) {
     }
 }
 
+// world debug_mode (marl_env.py:645-656): get_L2_state of the stepped books
+// (JaxOrderBookArrays.py:1231-1264) and the step's trade log.  Ten ascending-unique passes per
+// side: level k = the least key above level k-1 (the whole side for k = 0), a missing level
+// takes jnp.unique's fill; volumes get_volume_at_price at the level's (replaced) price.
+// bid key -p (an empty row's -1 is the level 1), fill 1, then -1 -> -maxint; ask key p with
+// -1 -> maxint, fill -1, then -1 -> maxint.  Negative volumes read 0.
+template <bool BID, int S>
+DEV i32 l2_side(const Side<S>& s, int R, const Valid<S>& V, i32 maxint, i32 outv) {
+    const int l = lane_id();
+    i32 x[S], q[S];
+    ldcol(s.t, R, FQ, q);
+#pragma unroll
+    for (int r = 0; r < S; ++r) x[r] = BID ? wmul(-1, s.pc[r]) : (s.pc[r] == -1 ? maxint : s.pc[r]);
+    i32 prev = 0;
+    for (int k = 0; k < HFTLOB_L2_LEVELS; ++k) {
+        i32 m = INT_MAX;
+        lmask any = 0;
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const bool ok = V.v[r] && (k == 0 || x[r] > prev);
+            m = imin_(m, ok ? x[r] : INT_MAX);
+            any |= bal(ok);
+        }
+        i32 lv = wave_min(m);
+        if (any == 0ull) lv = BID ? 1 : -1;
+        else prev = lv;
+        i32 p = BID ? wmul(-1, lv) : lv;
+        p = p == -1 ? (BID ? wsub(0, maxint) : maxint) : p;
+        i32 v = 0;
+#pragma unroll
+        for (int r = 0; r < S; ++r) v = wadd(v, (V.v[r] && s.pc[r] == p) ? q[r] : 0);
+        const i32 vol = imax_(wave_sum(v), 0);
+        const int c = k * 4 + (BID ? 2 : 0);
+        outv = l == c ? p : (l == c + 1 ? vol : outv);
+    }
+    return outv;
+}
+template <int S> DEV void write_debug(const Book<S>& B, i32* dst) {
+    const int l = lane_id(), R = B.c.nO;
+    i32 v = 0;
+    v = l2_side<false>(B.a, R, B.vs, B.c.maxint, v);
+    v = l2_side<true>(B.b, R, B.vs, B.c.maxint, v);
+    if (l < 4 * HFTLOB_L2_LEVELS) dst[l] = v;
+    store_trades(B.tr, dst + 4 * HFTLOB_L2_LEVELS, B.vt);
+}
+
 // ====================================================== K2: fused env step
 // MARLEnv.step — marl_env.py:775-804 (step_env :211-709, auto-reset select)
 #define MAX_AGENT_ROWS 128
@@ -2251,7 +2298,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                       const i32* __restrict__ init_states, i32* __restrict__ state, float* __restrict__ obs_out,
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
                       i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
-                      i32* lds, bool resident, bool keep, u32& fl_carry) {
+                      i32* __restrict__ debug_out, i32* lds, bool resident, bool keep, u32& fl_carry) {
     STAMP(t_start);
 #ifdef HFTLOB_STAMPS
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the in-kernel clock
@@ -2537,6 +2584,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     WorldView wv;
     wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
     wv.vol_a = side_volume(B.a, R, B.vs); wv.vol_b = side_volume(B.b, R, B.vs);
+    if (debug_out) write_debug(B, debug_out + (size_t)e * HFTLOB_DEBUG_WORDS(B.c.nT));  // before store / reset
     // the book is final: store it now (frees its registers for the rewards).  Not when the
     // auto-reset below rewrites the record anyway, nor while the wave's next step (keep,
     // k_env_rollout) takes the book and trade log from LDS as they are
@@ -2688,7 +2736,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
     u32 fl = 0;
     env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master != nullptr, mk, actions_io, msg_data, init_states,
                               state, out.obs, out.rewards, out.done_all, out.dones, out.info, out.obs_raw, out.msgs,
-                              lds, false, false, fl);
+                              out.debug, lds, false, false, fl);
     if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
 
@@ -2736,7 +2784,9 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
             out.dones + o * cc.n_agents, out.info ? out.info + o * cc.info_words : nullptr,
             out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
-            out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr, lds, NFIX > 0 && resident, NFIX > 0 && t + 1 < n_steps, fl);
+            out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr,
+            out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds, NFIX > 0 && resident,
+            NFIX > 0 && t + 1 < n_steps, fl);
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
     }
     if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
@@ -3100,6 +3150,7 @@ int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg, int n_env, int key_e0,
             so.info = out->info ? out->info + o * cfg->info_words : nullptr;
             so.obs_raw = out->obs_raw ? out->obs_raw + o * na * cfg->obs_stride : nullptr;
             so.msgs = out->msgs ? out->msgs + o * (size_t)cfg->n_msgs * 8 : nullptr;
+            so.debug = out->debug ? out->debug + o * (size_t)HFTLOB_DEBUG_WORDS(cfg->lob.n_trades) : nullptr;
             const uint32_t* kin = t == 0 ? key_in : kb + 2 * ((t - 1) & 1);
             uint32_t* kout = t == n_steps - 1 ? (g == 0 ? key_out : kb + 2 * (t & 1)) : kb + 2 * (t & 1);
             int32_t* acts = actions_out ? actions_out + o * cfg->action_words : nullptr;

@@ -12,7 +12,7 @@ import os
 from .layout import EnvCfg, LobCfg, StepOut
 
 LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
            "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_env_rollout_sampled", "hftlob_rollout_prepare",
            "hftlob_sample_actions", "hftlob_split_keys")

@@ -31,7 +31,8 @@ from .data.synthetic import LobsterDay, generate_day
 from .data.windows import Windows, init_messages, loaded_rows, make_windows
 from .engine import book_process_
 from .layout import (AGENT_MM, EXE_FLOAT, action_width, EXE_WORDS, INFO_AGENT_WORDS, INFO_EXE, INFO_MM, INFO_WORLD,
-                     INFO_WORLD_WORDS, MM_FLOAT, MM_WORDS, EnvLayout, StepOut, obs_fields, pack_env_cfg, trader_ids)
+                     INFO_WORLD_WORDS, L2_LEVELS, MM_FLOAT, MM_WORDS, EnvLayout, StepOut, debug_words, obs_fields,
+                     pack_env_cfg, trader_ids)
 
 
 # ------------------------------------------------------------------ spaces
@@ -197,6 +198,9 @@ class MARLEnv:
         # info["agents"][t]["obs_raw"] (marl_env.py:684-685): (field, dtype) per type, None = messages
         self.save_raw_observations = bool(w.save_raw_observations)
         self.obs_raw_fields = [obs_fields(a, w) for a in self.list_of_agents_configs]
+        # world debug_mode (marl_env.py:645-656): info["world"] also carries the step's trades, its
+        # combined messages and the 10-level lob_state of the stepped books
+        self.debug_mode = bool(w.debug_mode)
         self.return_info = return_info
         self.persistent_outputs = persistent_outputs
         self._out = None
@@ -262,6 +266,7 @@ class MARLEnv:
         """Output buffers of `lead` (E,) or (T, E) env steps and their hftlob_step_out."""
         L, dev, A = self.layout, self.device, self.num_agents
         want_raw = self.save_raw_observations and self.return_info
+        want_dbg = self.debug_mode and self.return_info
         o = {"obs": torch.empty(lead + (A, L.obs_stride), dtype=torch.float32, device=dev),
              "rewards": torch.empty(lead + (A,), dtype=torch.float32, device=dev),
              "done_all": torch.empty(lead, dtype=torch.bool, device=dev),
@@ -269,10 +274,12 @@ class MARLEnv:
              "info": torch.empty(lead + (L.info_words,), dtype=torch.int32, device=dev) if self.return_info else None,
              "obs_raw": torch.empty(lead + (A, L.obs_stride), dtype=torch.int32, device=dev) if want_raw else None,
              "msgs": torch.empty(lead + (L.n_msgs, 8), dtype=torch.int32, device=dev)
-             if any(self.message_obs_types) else None}
+             if any(self.message_obs_types) or want_dbg else None,
+             "debug": torch.empty(lead + (debug_words(L.n_trades),), dtype=torch.int32, device=dev)
+             if want_dbg else None}
         opt = lambda k: _lib.ptr(o[k]) if o[k] is not None else None  # noqa: E731
         o["struct"] = StepOut(_lib.ptr(o["obs"]), _lib.ptr(o["rewards"]), _lib.ptr(o["done_all"]),
-                              _lib.ptr(o["dones"]), opt("info"), opt("obs_raw"), opt("msgs"))
+                              _lib.ptr(o["dones"]), opt("info"), opt("obs_raw"), opt("msgs"), opt("debug"))
         return o
 
     def _split_types(self, x: torch.Tensor, obs: bool):
@@ -331,6 +338,11 @@ class MARLEnv:
         world = {n: col(k, isf) for k, (n, isf) in enumerate(INFO_WORLD)}
         world["time"] = torch.stack([world.pop("time_s"), world.pop("time_ns")], 1)
         world["current_step"] = world["step_counter"]
+        if o.get("debug") is not None:  # marl_env.py:645-656 (the stepped state's, as the rest of info)
+            n4 = 4 * L2_LEVELS
+            world["trades"] = o["debug"][:, n4:].reshape(E, self.layout.n_trades, 8)
+            world["total_msgs"] = o["msgs"]
+            world["lob_state"] = o["debug"][:, :n4]
         agents, a = [], 0
         for n_t in self.multi_agent_config.number_of_agents_per_type:
             fields = INFO_MM if self.layout.agent_kinds[a] == AGENT_MM else INFO_EXE

@@ -70,7 +70,16 @@ class EnvCfg(C.Structure):
 
 class StepOut(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("rewards", C.c_void_p), ("done_all", C.c_void_p),
-                ("dones", C.c_void_p), ("info", C.c_void_p), ("obs_raw", C.c_void_p), ("msgs", C.c_void_p)]
+                ("dones", C.c_void_p), ("info", C.c_void_p), ("obs_raw", C.c_void_p), ("msgs", C.c_void_p),
+                ("debug", C.c_void_p)]
+
+
+L2_LEVELS = 10                       # get_L2_state levels of world debug_mode (marl_env.py:646-651)
+
+
+def debug_words(n_trades: int) -> int:
+    """int32 words per env of the debug output: lob_state [10][4], then the trade log [nT][8]."""
+    return 4 * L2_LEVELS + 8 * n_trades
 
 
 # ----------------------------------------------------------- enum mappings

@@ -209,8 +209,12 @@ class IPPOTrainer:
         self.gen.manual_seed(c["SEED"] + 1000 * rank)
         self.params = env.default_params
         self._split = getattr(env, "split_keys", split_keys)   # device threefry split (jax.random.split)
-        # rng = PRNGKey(SEED); rng, _rng = split(rng); reset_rng = split(_rng, NUM_ENVS), sharded over
-        # the ranks in order (:283-284, 329); each rank then draws its step keys from its own rng
+        # rng = PRNGKey(SEED); rng, _rng = split(rng); reset keys = split(_rng, NUM_ENVS), sharded over
+        # the ranks in order; each rank then draws its step keys from its own rng.  This follows the
+        # SHAPE of the reference's key chain (:283-284, 329) but not its values: the reference also
+        # splits rng once per agent type for the network init (:246) before the reset split, and
+        # draws the per-device rngs as split(split(rng)[1], N_DEVICES) (:775-776).  The networks are
+        # torch-initialised here, so the same SEED gives different reset / step keys than JAX.
         master = torch.tensor([[0, c["SEED"]]], dtype=torch.int32, device=self.device)
         k = self._split(master, 2)[0]
         self.rng = (k[0] if world == 1 else self._split(k[0:1].contiguous(), world)[0][rank]).clone()

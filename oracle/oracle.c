@@ -1466,10 +1466,53 @@ int oracle_env_reset(const hftlob_env_cfg* c, int n_env, const u32* keys, const 
     return HFTLOB_OK;
 }
 
+/* ---- get_L2_state — JaxOrderBookArrays.py:1231-1264 (world debug_mode, marl_env.py:645-656).
+ * bid levels: -unique(-bid_prices, size=n, fill_value=1) (an empty row's -1 is a level, the fill
+ * reads -1), then -1 -> -maxint; ask levels: unique(where(p == -1, maxint, p), size=n,
+ * fill_value=-1), then -1 -> maxint; volumes get_volume_at_price at the (replaced) level price,
+ * negatives -> 0; out [n][4] = [ask_p, ask_q, bid_p, bid_q] (hstack((asks.T, bids.T)).flatten()). */
+static int cmp_i32(const void* a, const void* b) {
+    i32 x = *(const i32*)a, y = *(const i32*)b;
+    return (x > y) - (x < y);
+}
+static void unique_sorted(i32* v, int n, int size, i32 fill, i32* out) {
+    qsort(v, (size_t)n, sizeof(i32), cmp_i32);
+    int k = 0;
+    for (int i = 0; i < n && k < size; ++i)
+        if (i == 0 || v[i] != v[i - 1]) out[k++] = v[i];
+    for (; k < size; ++k) out[k] = fill;
+}
+static i32 volume_at(const i32* s, int nO, i32 p) {
+    i32 v = 0;
+    for (int i = 0; i < nO; ++i) if (s[i * 6] == p) v = wadd(v, s[i * 6 + 1]);
+    return v;
+}
+void oracle_l2_state(const hftlob_lob_cfg* c, const i32* asks, const i32* bids, int n_levels, i32* out) {
+    int nO = c->n_orders;
+    i32 tmp[HFTLOB_MAX_SLOTS], lv[HFTLOB_MAX_SLOTS];
+    for (int i = 0; i < nO; ++i) tmp[i] = wmul(-1, bids[i * 6]);
+    unique_sorted(tmp, nO, n_levels, 1, lv);
+    for (int k = 0; k < n_levels; ++k) {
+        i32 p = wmul(-1, lv[k]);
+        p = p == -1 ? wsub(0, c->maxint) : p;
+        i32 q = volume_at(bids, nO, p);
+        out[k * 4 + 2] = p;
+        out[k * 4 + 3] = q < 0 ? 0 : q;
+    }
+    for (int i = 0; i < nO; ++i) tmp[i] = asks[i * 6] == -1 ? c->maxint : asks[i * 6];
+    unique_sorted(tmp, nO, n_levels, -1, lv);
+    for (int k = 0; k < n_levels; ++k) {
+        i32 p = lv[k] == -1 ? c->maxint : lv[k];
+        i32 q = volume_at(asks, nO, p);
+        out[k * 4] = p;
+        out[k * 4 + 1] = q < 0 ? 0 : q;
+    }
+}
+
 /* ---- MARLEnv.step — marl_env.py:775-804 + step_env :211-709 */
 static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act, const i32* msg_data,
                          const i32* init_states, i32* rec, float* obs, float* rew, i32* done_all, i32* dones,
-                         i32* info, i32* obs_raw, i32* msgs_out) {
+                         i32* info, i32* obs_raw, i32* msgs_out, i32* debug) {
     Env E = {c, rec};
     int part = c->prng_partitionable, M = c->n_msgs, D = c->n_data_msg, A = c->n_action_msgs,
         C = c->n_cancel_msgs, nO = c->lob.n_orders, nT = c->lob.n_trades;
@@ -1585,6 +1628,10 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     float old_mid = bitf(W[3]);
     (void)old_mid;
     i32 ot0 = W[0], ot1 = W[1];
+    if (debug) { /* world debug_mode: lob_state of the stepped books, then the step's trades */
+        oracle_l2_state(&c->lob, asks, bids, HFTLOB_L2_LEVELS, debug);
+        memcpy(debug + 4 * HFTLOB_L2_LEVELS, trades, (size_t)nT * 8 * sizeof(i32));
+    }
     memcpy(ASKS(&E), asks, (size_t)nO * 6 * sizeof(i32));
     memcpy(BIDS(&E), bids, (size_t)nO * 6 * sizeof(i32));
     memcpy(TRADES(&E), trades, (size_t)nT * 8 * sizeof(i32));
@@ -1659,10 +1706,11 @@ static void env_step_one(const hftlob_env_cfg* c, const u32* key, const i32* act
     if (all) env_reset_one(c, key_reset, init_states, rec, obs);
 }
 
-int oracle_env_step_ex(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
-                       const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
-                       i32* info, i32* obs_raw, i32* msgs) {
+int oracle_env_step_dbg(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
+                        const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
+                        i32* info, i32* obs_raw, i32* msgs, i32* debug) {
     if (!env_cfg_ok(c)) return HFTLOB_EINVAL;
+    const size_t dw = (size_t)HFTLOB_DEBUG_WORDS(c->lob.n_trades);
 #pragma omp parallel for schedule(dynamic, 16)
     for (int e = 0; e < n_env; ++e)
         env_step_one(c, keys + 2 * e, actions + (size_t)e * c->action_words, msg_data, init_states,
@@ -1670,8 +1718,14 @@ int oracle_env_step_ex(const hftlob_env_cfg* c, int n_env, const u32* keys, cons
                      rew + (size_t)e * c->n_agents, done_all + e, dones + (size_t)e * c->n_agents,
                      info ? info + (size_t)e * c->info_words : NULL,
                      obs_raw ? obs_raw + (size_t)e * c->n_agents * c->obs_stride : NULL,
-                     msgs ? msgs + (size_t)e * c->n_msgs * 8 : NULL);
+                     msgs ? msgs + (size_t)e * c->n_msgs * 8 : NULL, debug ? debug + (size_t)e * dw : NULL);
     return HFTLOB_OK;
+}
+int oracle_env_step_ex(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
+                       const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
+                       i32* info, i32* obs_raw, i32* msgs) {
+    return oracle_env_step_dbg(c, n_env, keys, actions, msg_data, init_states, state, obs, rew, done_all, dones, info,
+                               obs_raw, msgs, NULL);
 }
 int oracle_env_step(const hftlob_env_cfg* c, int n_env, const u32* keys, const i32* actions, const i32* msg_data,
                     const i32* init_states, i32* state, float* obs, float* rew, i32* done_all, i32* dones,
@@ -1803,7 +1857,7 @@ int oracle_rollout_sampled(const hftlob_env_cfg* c, int n_env, int key_e0, int k
             u32 key[2];
             oracle_split(chain + 2 * t, key_n + 1, key_e0 + e + 1, part, key);
             oracle_sample_actions(c, 1, key, acts);
-            env_step_one(c, key, acts, msg_data, init_states, rec, obs, rew, &done_all, dones, NULL, NULL, NULL);
+            env_step_one(c, key, acts, msg_data, init_states, rec, obs, rew, &done_all, dones, NULL, NULL, NULL, NULL);
         }
     }
     master[0] = chain[2 * n_steps];

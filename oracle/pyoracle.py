@@ -28,6 +28,8 @@ def _bind(L):
     L.oracle_env_reset.argtypes = [vp, C.c_int, vp, vp, vp, vp]
     L.oracle_env_step.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_env_step_ex.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.oracle_env_step_dbg.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.oracle_l2_state.argtypes = [vp, vp, vp, C.c_int, vp]
     L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
     L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp]
     L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
@@ -117,10 +119,11 @@ def env_reset(env_cfg, keys, init_states):
     return state, obs
 
 
-def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=True, extras=False):
+def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=True, extras=False, debug=False):
     """Returns (state', obs, rewards, done_all, dones, info); `state` is not modified.
     extras: also return obs_raw (int32 words [E, n_agents, obs_stride], save_raw_observations)
-    and msgs (int32 [E, M, 8], the step's combined messages)."""
+    and msgs (int32 [E, M, 8], the step's combined messages).  debug: also return the world
+    debug_mode words (int32 [E, 40 + 8 * nTrades]: lob_state, then the step's trades) last."""
     keys = np.ascontiguousarray(keys, dtype=np.uint32).reshape(-1, 2)
     E = keys.shape[0]
     actions = np.ascontiguousarray(actions, dtype=np.int32).reshape(E, env_cfg.action_words)
@@ -132,13 +135,21 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
     info = np.zeros((E, env_cfg.info_words), dtype=np.int32) if with_info else None
     raw = np.zeros((E, env_cfg.n_agents, env_cfg.obs_stride), dtype=np.int32) if extras else None
     msgs = np.zeros((E, env_cfg.n_msgs, 8), dtype=np.int32) if extras else None
-    _chk(lib().oracle_env_step_ex(C.byref(env_cfg), E, _p(keys), _p(actions),
-                                  _p(np.ascontiguousarray(msg_data, np.int32)),
-                                  _p(np.ascontiguousarray(init_states, np.int32)), _p(st), _p(obs), _p(rew), _p(da),
-                                  _p(dn), _p(info), _p(raw), _p(msgs)))
-    if extras:
-        return st, obs, rew, da, dn, info, raw, msgs
-    return st, obs, rew, da, dn, info
+    dbg = np.zeros((E, 40 + 8 * env_cfg.lob.n_trades), dtype=np.int32) if debug else None
+    _chk(lib().oracle_env_step_dbg(C.byref(env_cfg), E, _p(keys), _p(actions),
+                                   _p(np.ascontiguousarray(msg_data, np.int32)),
+                                   _p(np.ascontiguousarray(init_states, np.int32)), _p(st), _p(obs), _p(rew), _p(da),
+                                   _p(dn), _p(info), _p(raw), _p(msgs), _p(dbg)))
+    out = (st, obs, rew, da, dn, info) + ((raw, msgs) if extras else ())
+    return out + (dbg,) if debug else out
+
+
+def l2_state(lob_cfg, asks, bids, n_levels=10):
+    """get_L2_state (JaxOrderBookArrays.py:1231-1264) of one book: int32 [n_levels * 4]."""
+    out = np.zeros(n_levels * 4, np.int32)
+    lib().oracle_l2_state(C.byref(lob_cfg), _p(np.ascontiguousarray(asks, np.int32)),
+                          _p(np.ascontiguousarray(bids, np.int32)), int(n_levels), _p(out))
+    return out
 
 
 def mm_action_msgs(env_cfg, type_idx, agent, rec, action):

@@ -95,3 +95,18 @@ def top_streams(n_env, n_msg, seed, price0=1000, maxint=2**31 - 1):
                 price = price0 - side * 5
             out[e, k] = (typ, side, qty, price, oid, tid, t, tn)
     return out
+
+
+def neg1_trade_streams(n_env, n_msg, seed, price0=1000):
+    """top_streams whose crossing messages (type 4 and the deep marketable limits) often carry
+    oid == -1 or time == -1.  match_order (JaxOrderBookArrays.py:205) writes a trade into the
+    first row whose col 4 (the message TIME, TradesFeat.SEC) is -1, so a trade made by a
+    time == -1 message leaves its row free for the next trade, while an oid == -1 one does not."""
+    out = top_streams(n_env, n_msg, seed, price0)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    crossing = (out[..., 0] == 4) | ((out[..., 0] == 1) & (np.abs(out[..., 3] - price0) == 5))
+    u = rng.random(out.shape[:2])
+    out[..., 4] = np.where(crossing & (u < 0.3), -1, out[..., 4])
+    out[..., 6] = np.where(crossing & (u >= 0.3) & (u < 0.6), -1, out[..., 6])
+    out[..., 7] = np.where(crossing & (u >= 0.5) & (u < 0.6), -1, out[..., 7])
+    return out

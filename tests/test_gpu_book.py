@@ -9,7 +9,7 @@ from hftlob.config import JAXLOB_Configuration
 from hftlob.engine import book_process_, scan_through_entire_array_save_bidask
 from hftlob.layout import pack_lob_cfg
 from oracle import pyoracle as O
-from streams import init_book_messages, random_streams, top_streams
+from streams import init_book_messages, neg1_trade_streams, random_streams, top_streams
 
 pytestmark = pytest.mark.gpu
 
@@ -107,5 +107,23 @@ def test_book_top_of_book_cache(kw):
     empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
     a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
     msgs = top_streams(E, M, seed=11 + cfg.nOrders)
+    _run(cfg, msgs, a0, b0, empty_t)
+    _run(cfg, msgs, empty_a, empty_a, empty_t)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(nOrders=16, nTrades=8), dict(nOrders=40, nTrades=30)],
+                         ids=["default", "nO16_nT8", "nO40_nT30"])
+def test_book_trade_row_neg1_fields(kw):
+    """Crossing messages with oid == -1 or time == -1 (streams.neg1_trade_streams): the trade log's
+    next row is the first whose col 4 (the trade's TIME) is -1 (JaxOrderBookArrays.py:205), so
+    a time == -1 trade is overwritten by the next one and an oid == -1 trade is kept."""
+    cfg = JAXLOB_Configuration(**kw)
+    E, M = 64, 400
+    init = init_book_messages(E, seed=6)
+    empty_a = np.full((E, cfg.nOrders, 6), -1, np.int32)
+    empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
+    a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
+    msgs = neg1_trade_streams(E, M, seed=21 + cfg.nOrders)
+    assert ((msgs[..., 4] == -1) & (msgs[..., 0] == 4)).any() and ((msgs[..., 6] == -1) & (msgs[..., 0] == 4)).any()
     _run(cfg, msgs, a0, b0, empty_t)
     _run(cfg, msgs, empty_a, empty_a, empty_t)

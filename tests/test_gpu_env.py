@@ -226,6 +226,24 @@ def _loaded(ep_type, tmp_root):
     return Lb.LoadedDay.from_arrays(*ld.run_loading("gpu_ft"))
 
 
+@pytest.mark.parametrize("nT", [100, 8])
+def test_env_trade_rows_neg1_fields(nT):
+    """Replayed executions (type 4) with order id -1 or time -1: the step's trade log takes its next
+    row at the first col 4 (TIME) == -1 (JaxOrderBookArrays.py:205), so trades of time -1 messages
+    are overwritten and those of oid -1 messages kept; nT = 8 also overflows the log every step."""
+    cfg = builtin_config("2_player_fq_fqc")
+    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, nTrades=nT))
+    base = _day(cfg.world_config, 2_000_000)
+    msgs = base.msgs.copy()
+    rng = np.random.Generator(np.random.PCG64(7))
+    u = rng.random(len(msgs))
+    ex = msgs[:, 0] == 4
+    msgs[:, 4] = np.where(ex & (u < 0.3), -1, msgs[:, 4])
+    msgs[:, 6] = np.where(ex & (u >= 0.3) & (u < 0.6), -1, msgs[:, 6])
+    day = dataclasses.replace(base, msgs=msgs)
+    rollout_parity(cfg, E=32, K=66, day=day)
+
+
 @pytest.mark.parametrize("ep_type", ["fixed_steps", "fixed_time"])
 def test_env_rollout_parity_lobster_loaded(ep_type, tmp_path_factory):
     """Raw LOBSTER files -> loader -> env: fixed_steps windows, and fixed_time windows with the

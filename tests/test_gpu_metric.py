@@ -60,11 +60,13 @@ def test_metric_shape_rollout_parity(mid, G):
 
 def test_rollout_shards_equal_whole_batch():
     """bench.py --gpus N: rank r steps envs [r*E, (r+1)*E) with key_e0 = r*E, key_n = N*E; the
-    shards together are the whole-batch rollout, bit for bit (state and carried key)."""
+    shards together are the whole-batch rollout, bit for bit (state and carried key).  The shards
+    run the persistent launch (n_slices 0, the bench's default at 4096 envs per GPU) and 1 / 2
+    slices, over 70 steps so every env crosses its episode end."""
     cfg = builtin_config("2_player_fq_fqc")
     env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000), persistent_outputs=True)
     params = env.default_params
-    E, N, T = 48, 3, 12
+    E, N, T = 48, 3, 70
     keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device="cuda"), N * E + 1)[0]
     _, whole = env.reset(keys[1:].contiguous(), params)
     shards = [env._wrap(whole.buf[r * E:(r + 1) * E].clone()) for r in range(N)]
@@ -72,7 +74,7 @@ def test_rollout_shards_equal_whole_batch():
     env.rollout_sampled(keys[0].clone(), kout, whole, params, T, n_slices=2)
     for r, s in enumerate(shards):
         ko = torch.empty(2, dtype=torch.int32, device="cuda")
-        env.rollout_sampled(keys[0].clone(), ko, s, params, T, n_slices=1 + r % 2, key_e0=r * E, key_n=N * E)
+        env.rollout_sampled(keys[0].clone(), ko, s, params, T, n_slices=r % 3, key_e0=r * E, key_n=N * E)
         assert (ko == kout).all(), f"rank {r}: carried key"
         assert (s.buf == whole.buf[r * E:(r + 1) * E]).all(), f"rank {r}: state"
 
