@@ -615,6 +615,7 @@ struct Book {
     // -1: the log loaded from memory has no such prefix shape; match_order then searches it.
     i32 ntr;
     bool part;
+    i32* filt;  // LDS: the 2048-bit id / init-price filter of chunk_noops (64 words)
 };
 
 // message handler codes (the reference's dispatch index) and flags, see decode_msgs
@@ -1081,14 +1082,150 @@ template <int S> DEV void refresh_best(Book<S>& B) {
     }
 }
 
+// ------------------------------------------------- chunk pre-pass: no-op messages
+// Which of a chunk's messages provably leave the book as it is, decided for the 64 messages at
+// once in VALU before the serial loop; the loop skips them and their best-quote record is the
+// previous message's (the book, hence get_best_* and get_volume_at_price, is unchanged).
+//  - doNothing rows (cond_type_side index 4: no branch of the lax.switch writes anything);
+//  - on a FAST book (both sides clean, no -1 oddities, the kernels' common variant) and before
+//    the first message that can end it: a cancel of quantity 0 (cancel_order subtracts 0 from
+//    whichever row it picks, JaxOrderBookArrays.py:93-139), and the replayed day's common cancel
+//    (DESIGN.md §4): an order id no row holds, no get_init_id_match candidate at its price, so
+//    the -1 index wraps to the last slot (:132-139) which is an all -1 row and stays one until
+//    the message (fewer adds to that side before it than free rows below the last slot, and only
+//    adds fill rows), and a quantity >= -1: q = -1 - qty <= 0 and _removeZeroNegQuant (:85-90)
+//    restores the all -1 row.
+// "No row holds the id / no candidate at the price" is a one-hash Bloom filter over the book's
+// ids and init-id rows' (price, side) at chunk start plus the chunk's add ids: a false positive
+// only means the message runs.  A message that can end the FAST variant or create a candidate
+// (an add with a -1 field, priced -1 or carrying an init id; a cancel of a negative quantity,
+// which can leave q > 0 in an empty row) ends the skipping for the rest of the chunk.
+DEV u32 hash_id(i32 v) { return ((u32)v * 0x9E3779B1u) >> 21; }
+DEV u32 hash_px(i32 p, bool ask) { return (((u32)p * 0x85EBCA6Bu) ^ (ask ? 0xC2B2AE35u : 0x27D4EB2Fu)) >> 21; }
+DEV void filt_set(i32* f, u32 h, bool on) {
+    __hip_atomic_fetch_or(reinterpret_cast<u32*>(f) + (h >> 5), on ? 1u << (h & 31) : 0u, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+DEV u32 filt_get(const i32* f, u32 h) { return ((u32)f[h >> 5] >> (h & 31)) & 1u; }
+DEV u32 lanes_below(lmask m) { return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)); }
+// -1 if the side's last slot is not an all -1 row, else the number of p == -1 rows below it
+template <int S> DEV int side_room(const Book<S>& B, const Side<S>& s) {
+    const int R = B.c.nO, rl = (R - 1) >> 6, ll = (R - 1) & 63;
+    int n = 0;
+    bool last = false;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        lmask f = B.vs.m[r] & bal(s.pc[r] == -1);
+        if (r == rl) {
+            last = (f >> ll) & 1ull;
+            f &= ~(1ull << ll);
+        }
+        n += __builtin_popcountll(f);
+    }
+    if (!last) return -1;
+    return ldu(s.t, R, FQ, R - 1) == -1 ? n : -1;
+}
+// x, y: the chunk's decoded messages (decode_msgs), lane = message; cnt: messages in the chunk
+template <bool RC, int S> DEV lmask chunk_noops(const Book<S>& B, const int4& x, const int4& y, int cnt) {
+    const int l = lane_id();
+    const i32 kind = x.x & H_KIND, qty = x.z, price = x.w, oid = y.x;
+    const bool in = l < cnt;
+    const lmask nop = bal(in & (kind == H_NOP));
+    if ((i32)B.fl >= 0) return nop;  // not FAST
+    const bool cnl = (kind == H_CNL_ASK) | (kind == H_CNL_BID), add = (kind == H_ASK) | (kind == H_BID);
+    const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
+    const u32 span = (u32)wsub(B.c.init_id, lo);
+    const bool init_oid = (u32)wsub(oid, lo) <= span;
+    const lmask brk = bal(in & ((add & (((x.x & (H_NEG1 | H_PM1)) != 0) | init_oid)) | (cnl & (qty < -1))));
+    const lmask before = brk ? (1ull << ff1(brk)) - 1ull : ~0ull;
+    const lmask zero = bal(in & cnl & (qty == 0)) & before;
+    if (RC || (u32)wsub(-1, lo) <= span) return nop | zero;  // (-1 ids would be init-id candidates)
+    i32* f = B.filt;
+    f[l] = 0;
+    lds_order();
+    const int R = B.c.nO;
+#pragma unroll
+    for (int sd = 0; sd < 2; ++sd) {
+        const Side<S>& s = sd ? B.b : B.a;
+        i32 o[S];
+        ldcol(s.t, R, FOID, o);
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            filt_set(f, hash_id(o[r]), B.vs.v[r] & (o[r] != -1));
+            filt_set(f, hash_px(s.pc[r], sd == 0), B.vs.v[r] & ((u32)wsub(o[r], lo) <= span));
+        }
+    }
+    filt_set(f, hash_id(oid), in & add);
+    lds_order();
+    const bool ask = kind == H_CNL_ASK;
+    const bool hit = (filt_get(f, hash_id(oid)) | filt_get(f, hash_px(price, ask))) != 0u;
+    const int room_a = side_room(B, B.a), room_b = side_room(B, B.b);
+    const u32 adds_a = lanes_below(bal(in & (kind == H_ASK))), adds_b = lanes_below(bal(in & (kind == H_BID)));
+    const int room = ask ? room_a : room_b;
+    const i32 adds = (i32)(ask ? adds_a : adds_b);
+    const bool quiet = in & cnl & (qty >= -1) & (oid != -1) & !hit & (room >= 0) & (adds <= room);
+    return nop | zero | (bal(quiet) & before);
+}
+
+// One chunk of the message scan: the chunk's messages that are not no-ops (chunk_noops) through
+// the book in order, each followed by its best-quote record (lane k of rpa / rqa / rpb / rqb:
+// get_best_ask / its volume, get_best_bid / its volume after message k); a skipped message
+// records the quotes after the message before it.  base: the chunk's first message index.
+template <bool RC, int S>
+DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, i32& rpa, i32& rqa, i32& rpb,
+                   i32& rqb) {
+    const lmask live = cnt >= 64 ? ~0ull : (1ull << cnt) - 1ull;
+#ifdef HFTLOB_NO_SKIP  // A/B builds only
+    const lmask skip = 0;
+#else
+    const lmask skip = chunk_noops<RC>(B, x, y, cnt) & live;
+#endif
+    lmask todo = live & ~skip;
+    refresh_best(B);
+    const i32 cpa = B.a.best_p, cqa = B.a.best_q, cpb = B.b.best_p, cqb = B.b.best_q;  // before the chunk
+    if (todo) {
+        // message k's fields are read (v_readlane) at the end of the message before it, so their
+        // latency overlaps the best-quote record and the loop test instead of stalling the dispatch
+        u32 k = ff1(todo);
+        i32 h = rdl(x.x, k), d1 = rdl(x.y, k), d2 = rdl(x.z, k), d3 = rdl(x.w, k), d4 = rdl(y.x, k),
+            d5 = rdl(y.y, k), d6 = rdl(y.z, k), d7 = rdl(y.w, k);
+        do {
+            asm volatile("s_bitset0_b64 %0, %1" : "+s"(todo) : "s"(k));
+            if (RC) B.mi = base + (int)k;
+            process_msg<RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
+            refresh_best(B);
+            const u32 kn = ff1(todo) & 63u;
+            h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
+            d4 = rdl(y.x, kn); d5 = rdl(y.y, kn); d6 = rdl(y.z, kn); d7 = rdl(y.w, kn);
+            rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
+            rpb = wlane(rpb, B.b.best_p, k); rqb = wlane(rqb, B.b.best_q, k);
+            k = kn;
+        } while (todo);
+    }
+    if (skip) {  // the skipped lanes take the record of the last message run before them
+        const int l = lane_id();
+        const lmask m = live & ~skip & (~0ull >> (63 - l));
+        const int src = m ? 63 - __builtin_clzll(m) : -1;
+        const i32 gpa = __builtin_amdgcn_ds_bpermute(src << 2, rpa), gqa = __builtin_amdgcn_ds_bpermute(src << 2, rqa);
+        const i32 gpb = __builtin_amdgcn_ds_bpermute(src << 2, rpb), gqb = __builtin_amdgcn_ds_bpermute(src << 2, rqb);
+        const bool own = (skip >> l) & 1ull;
+        rpa = own ? (src < 0 ? cpa : gpa) : rpa;
+        rqa = own ? (src < 0 ? cqa : gqa) : rqa;
+        rpb = own ? (src < 0 ? cpb : gpb) : rpb;
+        rqb = own ? (src < 0 ? cqb : gqb) : rqb;
+    }
+}
+
 // LDS carve-up of one env's book: [asks 6*nO][bids 6*nO][trades 8*nT][pad 64*4]
-// (column loads may over-read up to 127 words past the trades: padding; the
-// last 64 pad words are the store scratch row)
+// (column loads read past the trades (lanes masked by Valid; up to 127 words at the 100/100
+// sizes): the first 128 pad words; then the chunk_noops filter (64 words) and the store scratch
+// row (64 words), which over-reads at small nT may also read)
 template <int S> DEV void book_bind(Book<S>& B, i32* lds) {
     B.a.t = lds;
     B.b.t = lds + 6 * B.c.nO;
     B.tr.t = lds + 12 * B.c.nO;
     B.tr.R = B.c.nT;
+    B.filt = lds + 12 * B.c.nO + 8 * B.c.nT + 128;
     B.a.scr = B.b.scr = B.tr.scr = lds + 12 * B.c.nO + 8 * B.c.nT + 192;
     B.vs.init(B.c.nO);
     B.vt.init(B.c.nT);
@@ -1150,16 +1287,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
         decode_msgs(B.c, x, y);
         i32 ap = 0, aq = 0, bp = 0, bq = 0;
         const int cnt = uni(imin_(64, n_msg - base));  // SGPR: the loop test stays on the scalar unit
-        for (int k = 0; k < cnt; ++k) {
-            if (RC) B.mi = base + k;
-            process_msg<RC>(B, rdl(x.x, k), rdl(x.y, k), rdl(x.z, k), rdl(x.w, k), rdl(y.x, k), rdl(y.y, k),
-                            rdl(y.z, k), rdl(y.w, k));
-            if (best_asks) {
-                refresh_best(B);
-                ap = wlane(ap, B.a.best_p, k); aq = wlane(aq, B.a.best_q, k);
-                bp = wlane(bp, B.b.best_p, k); bq = wlane(bq, B.b.best_q, k);
-            }
-        }
+        run_chunk<RC>(B, x, y, cnt, base, ap, aq, bp, bq);
         if (best_asks && row < n_msg) {
             reinterpret_cast<int2*>(best_asks + ((size_t)e * n_msg + row) * 2)[0] = make_int2(ap, aq);
             reinterpret_cast<int2*>(best_bids + ((size_t)e * n_msg + row) * 2)[0] = make_int2(bp, bq);
@@ -2529,20 +2657,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         decode_msgs(B.c, x, y);
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
         const int cnt = uni(imin_(64, M - base));  // SGPR: the loop test stays on the scalar unit
-        // message k + 1's fields are read (v_readlane) at the end of message k, so their latency
-        // overlaps the best-quote record and the loop test instead of stalling the dispatch
-        i32 h = rdl(x.x, 0), d1 = rdl(x.y, 0), d2 = rdl(x.z, 0), d3 = rdl(x.w, 0), d4 = rdl(y.x, 0),
-            d5 = rdl(y.y, 0), d6 = rdl(y.z, 0), d7 = rdl(y.w, 0);
-        for (int k = 0; k < cnt; ++k) {
-            if (RC) B.mi = base + k;
-            process_msg<RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
-            refresh_best(B);
-            const int kn = (k + 1) & 63;
-            h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
-            d4 = rdl(y.x, kn); d5 = rdl(y.y, kn); d6 = rdl(y.z, kn); d7 = rdl(y.w, kn);
-            rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
-            rpb = wlane(rpb, B.b.best_p, k); rqb = wlane(rqb, B.b.best_q, k);
-        }
+        run_chunk<RC>(B, x, y, cnt, base, rpa, rqa, rpb, rqb);
         // abort flag on raw quotes; _ffill_best_prices (marl_env.py:723-749) for the chunk
         abort_any |= bal((l < cnt) & ((rpa == -1) | (rpb == -1))) != 0ull;
         i32 pa = rpa, pb = rpb;
@@ -2751,6 +2866,40 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
 // still scalar loads, re-issued once per step.  (Never take &c: that copies the
 // struct to scratch.)
 typedef const __attribute__((address_space(4))) hftlob_env_cfg kcfg_t;
+
+// Issue priority by projected finish.  An env's work over a rollout depends on its data windows
+// (their crossings, full sides, cancels; tools/diag_wavetime.py measures a coefficient of variation
+// of the per-env time), and the launch ends with its slowest env, while the 16 waves of a CU share
+// the CU's scalar unit and each SIMD's issue slots.  After every step a wave projects its end
+// (100 MHz reference clock: elapsed / steps done * steps left), publishes it in the table slot of
+// its hardware wave slot and ranks itself among the live waves of its CU (slots whose projection
+// lies ahead of now; a finished wave's last projection is its end, in the past): the quarter due
+// last runs at s_setprio 3, the next at 2, and so on (the longest-remaining-first rule for a
+// makespan).  Slots are per hardware wave slot, so concurrent launches never share one; the table
+// is zero-initialised device memory of the code object (no allocation).  Scheduling only: no
+// result depends on it.
+#define WAVE_SLOTS (8 * 16 * 16 * 64)  // XCC (8) x SE (8) x SH (2) x CU (16), x 64 wave slots per CU
+__device__ unsigned long long g_wave_eta[WAVE_SLOTS];
+DEV void balance_prio(u32 hwid, u32 xcc, unsigned long long r0, int done, int left) {
+    const int l = lane_id();
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    const float el = (float)(now - r0);
+    const unsigned long long eta = now + (unsigned long long)(el * ((float)left / (float)done));
+    const u32 cu = ((xcc & 7u) * 16u + ((hwid >> 13) & 7u) * 2u + ((hwid >> 12) & 1u)) * 16u + ((hwid >> 8) & 15u);
+    const u32 slot = ((hwid >> 4) & 3u) * 16u + (hwid & 15u);
+    unsigned long long* row = g_wave_eta + (size_t)cu * 64u;
+    if (l == 0) __hip_atomic_store(row + slot, eta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long v = __hip_atomic_load(row + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = (u32)l == slot ? eta : v;
+    const lmask live = bal(v > now);
+    const lmask later = live & bal((v > eta) | ((v == eta) & ((u32)l < slot)));
+    const int n = __builtin_popcountll(live), rank = __builtin_popcountll(later);
+    const int q = n > 0 ? (4 * rank) / n : 0;  // 0: due last
+    if (q == 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 template <int S, int NFIX, bool RC>
 __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_env, int key_e0, int key_n, int n_steps,
                                                     int per_step, const u32* __restrict__ master,
@@ -2770,6 +2919,16 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
     // lane masks of the resident branch to VGPRs, which s_ff1's SGPR operand cannot take.)
     bool resident = false;
     u32 fl = 0;
+#ifndef HFTLOB_NO_BALANCE
+    const unsigned long long bal_r0 = __builtin_amdgcn_s_memrealtime();
+    const u32 bal_hwid = __builtin_amdgcn_s_getreg(0xF804), bal_xcc = __builtin_amdgcn_s_getreg(0x7814);
+#endif
+#ifdef HFTLOB_WAVETIME
+    // diagnostic build only (tools/diag_wavetime.py): the wave's start time and hardware slot,
+    // then each step's end time, into the per-step info rows (words 0..9 of row (t, e))
+    const unsigned long long wt_start = __builtin_amdgcn_s_memtime(), wt_rstart = __builtin_amdgcn_s_memrealtime();
+    const u32 wt_hwid = __builtin_amdgcn_s_getreg(0xF804), wt_xcc = __builtin_amdgcn_s_getreg(0x7814);
+#endif
 #pragma unroll 1
     for (int t = 0; t < n_steps; ++t) {
         const size_t o = per_step ? (size_t)t * n_env : 0;
@@ -2788,6 +2947,21 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
             out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds, NFIX > 0 && resident,
             NFIX > 0 && t + 1 < n_steps, fl);
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
+#ifndef HFTLOB_NO_BALANCE
+        if (t + 1 < n_steps) balance_prio(bal_hwid, bal_xcc, bal_r0, t + 1, n_steps - t - 1);
+#endif
+#ifdef HFTLOB_WAVETIME
+        if (out.info && per_step) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime(), rnow = __builtin_amdgcn_s_memrealtime();
+            const i32 w10[10] = {(i32)(u32)now, (i32)(u32)(now >> 32), (i32)wt_hwid, (i32)wt_xcc, (i32)(u32)wt_start,
+                                 (i32)(u32)(wt_start >> 32), (i32)(u32)rnow, (i32)(u32)(rnow >> 32),
+                                 (i32)(u32)wt_rstart, (i32)(u32)(wt_rstart >> 32)};
+            i32 v = 0;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) v = lane_id() == k ? w10[k] : v;
+            if (lane_id() < 10) out.info[((size_t)t * n_env + e) * cc.info_words + lane_id()] = v;
+        }
+#endif
     }
     if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
