@@ -10,12 +10,13 @@
   state0 and master_key.
 
 The K timed steps are one MARLEnv.rollout_sampled call (hftlob_env_rollout_sampled,
-Speed_test's whole scan): split + sample + step fused.  While the whole batch is resident on
-the GPU (the metric: 4096 envs, 16 one-wave workgroups per CU) that is ONE persistent
-k_env_rollout launch in which every env runs its K steps back to back with its book kept in
-LDS; larger batches run as 2 contiguous env slices on their own streams, one k_env_step launch
-per slice and step, so one slice's slowest envs overlap the other slice's next step
-(MARLEnv.default_slices; both bit-exact with K full-batch launches, tests/test_gpu_env.py).
+Speed_test's whole scan): split + sample + step fused.  By default (MARLEnv.default_slices)
+that is ONE persistent k_env_rollout launch while the whole batch is resident on the GPU (the
+metric: 4096 envs, 16 one-wave workgroups per CU): every env runs its K steps back to back with
+its book kept in LDS, each wave's issue priority ranked by its projected finish.  Batches that
+do not fit at once run as 2 contiguous env slices on their own streams, one k_env_step launch
+per slice and step, so one slice's slowest envs overlap the other slice's next step (both
+bit-exact with K full-batch launches, tests/test_gpu_env.py).
 --mode step: Speed_test's three calls (split_keys, sample_actions, env.step) as three launches
 per step.
 
@@ -374,17 +375,37 @@ def main(argv=None):
     if prof and prof.get("slices", 2) != args.slices:  # measured on another launch shape
         prof = None
     kernel = "k_env_rollout" if args.mode == "rollout" and args.slices == 0 else "k_env_step"
-    traffic = round(prof["hbm_bytes_per_env_step"] * E) if prof and prof.get("hbm_bytes_per_env_step") else None
+    # the profile's figures for this run's launch length (HBM bytes per env-step depend on it: the
+    # persistent launch loads the books once per launch); the nearest measured length otherwise
+    traffic, t_spl, rp = None, None, None
+    if prof:
+        by = prof.get("hbm_bytes_per_env_step_by_launch_steps") or (
+            {str(prof.get("traffic_steps_per_launch", prof.get("steps_per_launch", 1))): prof["hbm_bytes_per_env_step"]}
+            if prof.get("hbm_bytes_per_env_step") else {})
+        if by:
+            t_spl = min(by, key=lambda k: abs(int(k) - T))
+            traffic = round(by[t_spl] * E)
+            t_spl = int(t_spl)
+        rp = {k: prof[k] for k in ("kernel_avg_us", "launches", "steps_per_launch", "kernel_us_per_step",
+                                   "envs_per_launch", "launches_in_flight", "source") if k in prof}
+        r20 = prof.get("rocprof_20_step_launch")
+        if r20 and abs(T - 20) < abs(T - rp.get("steps_per_launch", T)):
+            rp = dict(rp, **r20)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                 "kernel": kernel, "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env,
                 "units_per_launch": E,
-                "launches_per_step": (args.slices or round(1 / T, 6)) if args.mode == "rollout" else 3}
+                "launches_per_step": (args.slices or round(1 / T, 6)) if args.mode == "rollout" else 3,
+                "limiter": ("issue / dependent latency, not HBM: the measured traffic is far below the algorithmic "
+                            "bytes (the books stay in LDS) and below the peak (measured_frac); see issue_roofline "
+                            "and DESIGN.md section 4")}
+    if traffic is not None:
+        roofline["traffic_steps_per_launch"] = t_spl
+        # the bandwidth the kernel really draws: counted HBM bytes per batched step / time per step
+        roofline["measured_frac"] = round(traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)
     issue = None
     if prof:
-        roofline["rocprof"] = {k: prof[k] for k in ("kernel_avg_us", "launches", "steps_per_launch",
-                                                    "kernel_us_per_step", "envs_per_launch", "launches_in_flight",
-                                                    "source") if k in prof}
+        roofline["rocprof"] = rp
         if prof.get("salu_per_env_step"):
             # the CU's one scalar ALU, shared by its waves, is the scarcest pipe
             a = prof["salu_per_env_step"] * world * E * args.steps / elapsed / N_CU / world

@@ -344,6 +344,11 @@ struct Side {
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid under F_OK
     i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
                          // every handler reads prices, only adds and row clears write them
+    // top-of-book cache: the slot _get_top_*_order_idx returns for max / min price top_p, and its
+    // (ts, tns); top = -1: unknown.  Kept across messages: a quantity change keeps it, clearing the
+    // row (or any bulk clear) drops it, an add at a better price or an earlier time at top_p
+    // replaces it (see top_new / top_eq), so a crossing message usually skips the top-of-book scan
+    i32 top, top_p, top_ts, top_tns;
 };
 
 // slot e of a lane-strided register column <- v (lane e & 63 of register e >> 6): one
@@ -422,6 +427,7 @@ DEV u32 commit_side(Side<S>& s, const SideRows<S>& f, int R, const Valid<S>& V) 
         pm1 |= V.m[r] & bal((p == -1) & (all0 != 0u));
     }
     lds_order();
+    s.top = -1;
     return (bad == 0ull ? SideBits<ASKS>::CLEAN : 0u) | (n1 != 0ull ? SideBits<ASKS>::NEG1 : 0u) |
            (pm1 != 0ull ? SideBits<ASKS>::PM1 : 0u);
 }
@@ -432,6 +438,7 @@ template <int S> DEV void relink_side(Side<S>& s, int R, const Valid<S>& V) {
     ldcol(s.t, R, FP, p);
 #pragma unroll
     for (int r = 0; r < S; ++r) s.pc[r] = V.v[r] ? p[r] : -1;
+    s.top = -1;
 }
 template <bool ASKS, int S> DEV u32 load_side(Side<S>& s, const i32* g, int R, const Valid<S>& V) {
     SideRows<S> f;
@@ -465,6 +472,7 @@ template <int S> DEV void clear_masked(Side<S>& s, int R, const lmask (&m)[S]) {
         }
     }
     lds_order();
+    s.top = -1;
 }
 
 // _removeZeroNegQuant — JaxOrderBookArrays.py:85-90 on a side that is not
@@ -519,7 +527,8 @@ template <bool ASKS, int S> DEV void rescan(Side<S>& s, u32& fl, int R, const Va
 // _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
 // mp is the side's max price (bid) / min price with -1 -> maxint (ask)
 template <int S>
-DEV int top_idx(const i32 (&p)[S], const i32 (&ts)[S], const i32 (&tns)[S], const Valid<S>& V, const LobCfg& c, i32 mp) {
+DEV int top_idx(const i32 (&p)[S], const i32 (&ts)[S], const i32 (&tns)[S], const Valid<S>& V, const LobCfg& c, i32 mp,
+                i32& mts_out, i32& mtn_out) {
     i32 t[S], n[S], m = INT_MAX;
 #pragma unroll
     for (int r = 0; r < S; ++r) {
@@ -534,6 +543,8 @@ DEV int top_idx(const i32 (&p)[S], const i32 (&ts)[S], const i32 (&tns)[S], cons
         m = imin_(m, V.v[r] ? n[r] : INT_MAX);
     }
     const i32 mtn = wave_min(m);
+    mts_out = mts;
+    mtn_out = mtn;
     lmask pm[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) pm[r] = V.m[r] & bal(n[r] == mtn);
@@ -628,35 +639,62 @@ struct Msg {
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
 // side: it changes (best_p, best_q) only where get_best_* / get_volume_at_price
 // would, and falls back to a full recompute (ok = false) where it cannot tell.
-template <bool BID, int S> DEV void note_add(Side<S>& s, u32& fl, i32 np, i32 nq, i32 maxint) {
-    // an all -1 row now holds (np, nq > 0).  Branches ordered for the common case, an order
-    // behind the best (one compare each); per side the cases are those of get_best_* with -1
-    // (and, for asks, maxint) standing for "no price".
+// the top-of-book cache after an order (np, t, tns) went to slot e:
+// a new best price: the row is alone at it, so it is the top (unless a maxint time, where the
+// top-of-book formula's maxint placeholders could tie with it)
+template <int S> DEV void top_new(Side<S>& s, int e, i32 np, i32 t, i32 tns, i32 maxint) {
+    s.top = ((t != maxint) & (tns != maxint)) ? e : -1;
+    s.top_p = np; s.top_ts = t; s.top_tns = tns;
+}
+// an order at the best price: the top moves to it only if it is earlier in (ts, tns, slot)
+// (a known top is at the best price, np: note_add drops it whenever the best quote is not known;
+// one branch per test, the common case first: an OR of the tests becomes 64-bit lane-mask logic
+// on the scalar unit)
+template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) {
+    if (fresh(t) > s.top_ts) return;  // a later order (the common case)
+    asm volatile("");
+    if (s.top < 0) return;
+    asm volatile("");
+    bool earlier = t < s.top_ts;
+    if (!earlier) earlier = (tns < s.top_tns) | ((tns == s.top_tns) & (e < s.top));
+    if (earlier) {
+        s.top = tns != maxint ? e : -1;  // (t < top_ts < maxint)
+        s.top_ts = t; s.top_tns = tns;
+    }
+}
+template <bool BID, int S>
+DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint) {
+    // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
+    // common case, an order behind the best (one compare each); per side the cases are those of
+    // get_best_* with -1 (and, for asks, maxint) standing for "no price".
     constexpr u32 OK = SideBits<!BID>::OK;
-    if (!(fl & OK)) return;
+    if (!(fl & OK)) { s.top = -1; return; }
     const i32 bp = s.best_p;
     if (BID) {
         if (np < bp) {
             if (bp == -1) fl &= ~OK;        // np < -1 on an empty side
         } else if (np > bp) {
             s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
+            top_new(s, e, np, t, tns, maxint);
         } else if (bp == -1) {
             fl &= ~OK;                      // np == -1 on an empty side
         } else {
             s.best_q = wadd(s.best_q, nq);
+            top_eq(s, e, t, tns, maxint);
         }
     } else {
         if (np > bp) {
             if (bp == -1) {                 // empty side
                 if (np == maxint) fl &= ~OK;
-                else { s.best_p = np; s.best_q = nq; }
+                else { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
             }
         } else if (np < bp) {
-            if (np != -1) { s.best_p = np; s.best_q = nq; }
+            if (np != -1) { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
         } else if (np == -1) {
             fl &= ~OK;
         } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
+            top_eq(s, e, t, tns, maxint);
         }
     }
 }
@@ -690,6 +728,7 @@ template <int S> DEV void side_put(Side<S>& s, int R, int e, i32 f0, i32 f1, i32
 template <int S> DEV void side_clr(Side<S>& s, int R, int e) {
     clr6(s.t, s.scr, R, e);
     col_set(s.pc, e, -1);
+    s.top = e == s.top ? -1 : s.top;
 }
 // the side's p == -1 slots (all -1 rows in the FAST variant)
 template <int S> DEV void free_slots(const Book<S>& B, const Side<S>& s, lmask (&free)[S]) {
@@ -768,12 +807,26 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
         } else if (mp < price) {
             break;
         }
-        i32 q[S], o[S], t[S], ts[S], tn[S];
-        ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
-        ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
-        const int top = top_idx(s.pc, ts, tn, B.vs, B.c, mp);
-        const i32 qt = sget(q, top), ot = sget(o, top), tt = sget(t, top);
-        const i32 tp = sget(s.pc, top);
+        int top;
+        i32 qt, ot, tt, tp;
+        if (s.top >= 0 && s.top_p == mp) {  // the cached top (a row at mp): three broadcast reads
+            top = s.top;
+            qt = ldu(s.t, R, FQ, top); ot = ldu(s.t, R, FOID, top); tt = ldu(s.t, R, FTID, top);
+            tp = mp;
+        } else {
+            i32 q[S], o[S], t[S], ts[S], tn[S], mts, mtn;
+            ldcol(s.t, R, FTS, ts); ldcol(s.t, R, FTNS, tn);
+            ldcol(s.t, R, FQ, q); ldcol(s.t, R, FOID, o); ldcol(s.t, R, FTID, t);
+            top = top_idx(s.pc, ts, tn, B.vs, B.c, mp, mts, mtn);
+            qt = sget(q, top); ot = sget(o, top); tt = sget(t, top); tp = sget(s.pc, top);
+            s.top_p = mp; s.top_ts = mts; s.top_tns = mtn;
+            // cached only when the formula picks the earliest row AT mp: if the earliest-ts rows
+            // at mp all have tns == maxint, the formula's maxint placeholders tie and it returns
+            // the side's first slot, whatever its price or time (a quirk kept bit for bit, which
+            // tests/streams.py::top_streams reaches)
+            s.top = ((tp == mp) & (mp != -1) & (mp != B.c.maxint) & (mts != B.c.maxint) & (mtn != B.c.maxint))
+                        ? top : -1;
+        }
         if (fresh(tp) == -1) break;  // (two branches, not a 64-bit lane-mask OR)
         asm volatile("");
         if (BID ? tp < price : tp > price) break;
@@ -796,8 +849,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         if (nq > 0) {
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
             if (m.h & (H_NEG1 | H_PM1)) B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
-            if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
-            else B.fl &= ~OK;
+            if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
+            else { B.fl &= ~OK; s.top = -1; }
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
             side_clr(s, R, e);
             B.fl &= ~OK;
@@ -832,8 +885,8 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         if (m.h & H_NEG1) B.fl |= NEG1;
         if (m.h & H_PM1) B.fl |= PM1;
-        if (was_empty) note_add<BID>(s, B.fl, m.price, nq, B.c.maxint);
-        else B.fl &= ~OK;
+        if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
+        else { B.fl &= ~OK; s.top = -1; }
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         side_clr(s, R, e);
         B.fl &= ~OK;
@@ -856,9 +909,11 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
     lmask m[S];
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = B.vs.m[r] & bal(s.pc[r] == worst);
+    const i32 top = s.top;
     clear_masked(s, R, m);
-    // only the worst level goes: the best quote survives unless the side holds one price level
-    // (worst == best; an ask side whose prices are all maxint has best -1)
+    // only the worst level goes: the best quote and the top of book survive unless the side holds
+    // one price level (worst == best; an ask side whose prices are all maxint has best -1)
+    s.top = worst != s.top_p ? top : -1;
     if ((worst == s.best_p) | (s.best_p == -1)) B.fl &= ~SideBits<!BID>::OK;
     free_slots(B, s, free);
 }
@@ -879,7 +934,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
     }
-    note_add<BID>(s, B.fl, m.price, qty, B.c.maxint);
+    note_add<BID>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
@@ -2870,12 +2925,14 @@ typedef const __attribute__((address_space(4))) hftlob_env_cfg kcfg_t;
 // Issue priority by projected finish.  An env's work over a rollout depends on its data windows
 // (their crossings, full sides, cancels; tools/diag_wavetime.py measures a coefficient of variation
 // of the per-env time), and the launch ends with its slowest env, while the 16 waves of a CU share
-// the CU's scalar unit and each SIMD's issue slots.  After every step a wave projects its end
-// (100 MHz reference clock: elapsed / steps done * steps left), publishes it in the table slot of
-// its hardware wave slot and ranks itself among the live waves of its CU (slots whose projection
-// lies ahead of now; a finished wave's last projection is its end, in the past): the quarter due
-// last runs at s_setprio 3, the next at 2, and so on (the longest-remaining-first rule for a
-// makespan).  Slots are per hardware wave slot, so concurrent launches never share one; the table
+// the CU's scalar unit and each SIMD's issue slots, and each SIMD's arbiter favours its oldest
+// wave: without a rule the 4 waves of a SIMD finish in dispatch order, the youngest last
+// (profiles/r03_wavetime_unbalanced.json: the live waves fall 4096 -> 3072 -> 2048 -> 1024).
+// After every step a wave projects its end (100 MHz reference clock: elapsed / steps done *
+// steps left), publishes it in the table slot of its hardware wave slot and ranks itself among
+// the live waves of its SIMD (slots whose projection lies ahead of now; a finished wave's last
+// projection is its end, in the past): the quarter due last runs at s_setprio 3, the next at 2,
+// and so on (the longest-remaining-first rule for a makespan).  Slots are per hardware wave slot, so concurrent launches never share one; the table
 // is zero-initialised device memory of the code object (no allocation).  Scheduling only: no
 // result depends on it.
 #define WAVE_SLOTS (8 * 16 * 16 * 64)  // XCC (8) x SE (8) x SH (2) x CU (16), x 64 wave slots per CU
@@ -2891,6 +2948,7 @@ DEV void balance_prio(u32 hwid, u32 xcc, unsigned long long r0, int done, int le
     if (l == 0) __hip_atomic_store(row + slot, eta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long v = __hip_atomic_load(row + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     v = (u32)l == slot ? eta : v;
+    v = ((u32)l >> 4) == (slot >> 4) ? v : 0ull;  // the wave's own SIMD (A/B: +2.6 % over the whole CU)
     const lmask live = bal(v > now);
     const lmask later = live & bal((v > eta) | ((v == eta) & ((u32)l < slot)));
     const int n = __builtin_popcountll(live), rank = __builtin_popcountll(later);

@@ -110,3 +110,87 @@ def neg1_trade_streams(n_env, n_msg, seed, price0=1000):
     out[..., 6] = np.where(crossing & (u >= 0.3) & (u < 0.6), -1, out[..., 6])
     out[..., 7] = np.where(crossing & (u >= 0.5) & (u < 0.6), -1, out[..., 7])
     return out
+
+
+def full_book_messages(n_env, seed, nO=100, lo=0.85, hi=1.0, price0=1000):
+    """Init messages that leave each side holding between lo * nO and hi * nO orders (per env and
+    side), at distinct prices behind the touch, a third of them with the init id (-2, the
+    get_init_id_match candidates): books whose last slot is occupied or not, and a few free rows,
+    for the no-op skip's room test."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rows = []
+    for e in range(n_env):
+        r = []
+        for side in (-1, 1):
+            n = int(rng.integers(int(lo * nO), int(hi * nO) + 1))
+            for k in range(n):
+                price = price0 - side * (3 + k) + (0 if side == 1 else 0)
+                oid = -2 if rng.random() < 0.33 else 100000 + 1000 * (side + 1) + k
+                r.append((1, side, int(rng.integers(1, 50)), price, oid, -2 - k, 34199, k))
+        rows.append(r)
+    m = max(len(r) for r in rows)
+    out = np.zeros((n_env, m, 8), dtype=np.int32)  # doNothing padding
+    for e, r in enumerate(rows):
+        out[e, :len(r)] = r
+    return out
+
+
+def noop_streams(n_env, n_msg, seed, price0=1000, nO=100):
+    """Streams for the chunk pre-pass that skips messages which leave the book unchanged
+    (hftlob.hip chunk_noops): mostly cancels of ids no row holds (the replayed day's common
+    cancel: its -1 index wraps to the last slot), at prices that do and do not hold init-id rows,
+    with quantities 1..50, 0, -1 (skippable) and below -1 (which end the skipping); doNothing rows;
+    cancels of live ids and of id -1; non-crossing adds that fill the last free rows of a side
+    (the room test's boundary), adds carrying an init id or a -1 field (which end the skipping),
+    and executions."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.zeros((n_env, n_msg, 8), dtype=np.int32)
+    for e in range(n_env):
+        live = []
+        next_oid = 20000
+        t, tn = 34200, 0
+        for k in range(n_msg):
+            tn += int(rng.integers(1, 500))
+            side = int(rng.choice([-1, 1]))
+            lvl = int(rng.integers(1, 12))
+            price = price0 - side * lvl
+            qty = int(rng.integers(1, 50))
+            tid = int(rng.integers(1, 6))
+            u = rng.random()
+            if u < 0.25:                      # non-crossing add
+                typ, oid = 1, next_oid
+                next_oid += 1
+                live.append((oid, side, price))
+            elif u < 0.62:                    # cancel of an id no row holds
+                typ = int(rng.choice([2, 3]))
+                oid = int(rng.integers(1, 10**6))
+                v = rng.random()
+                qty = 0 if v < 0.08 else (-1 if v < 0.14 else qty)
+            elif u < 0.70 and live:           # cancel of a live id
+                typ = int(rng.choice([2, 3]))
+                oid, side, price = live[int(rng.integers(0, len(live)))]
+            elif u < 0.75:                    # zero-quantity cancel
+                typ, oid, qty = 3, int(rng.integers(1, 10**6)), 0
+            elif u < 0.80:                    # doNothing row
+                typ, side, qty, price, oid, tid = 0, 0, 0, 0, 0, 0
+            elif u < 0.82:                    # cancel of id -1
+                typ, oid = int(rng.choice([2, 3])), -1
+                qty = int(rng.choice([1, 0, -1]))
+            elif u < 0.85:                    # init-id cancel (get_init_id_match candidates)
+                typ, oid = 2, -2 - int(rng.integers(0, 25))
+            elif u < 0.87:                    # add carrying an init id (ends the skipping)
+                typ, oid = 1, -2 - int(rng.integers(0, 21))
+            elif u < 0.89:                    # add with a -1 field (ends the FAST variant)
+                typ, oid, tid = 1, next_oid, -1
+                next_oid += 1
+            elif u < 0.90:                    # cancel of a negative quantity (ends the skipping)
+                typ, oid, qty = int(rng.choice([2, 3])), int(rng.integers(1, 10**6)), -int(rng.integers(2, 6))
+            elif u < 0.95:                    # execution
+                typ = 4
+                oid = live[int(rng.integers(0, len(live)))][0] if live else 7
+            else:                             # marketable limit
+                typ, oid = 1, next_oid
+                next_oid += 1
+                price = price0 + side * 4
+            out[e, k] = (typ, side, qty, price, oid, tid, t, tn)
+    return out

@@ -9,7 +9,7 @@ from hftlob.config import JAXLOB_Configuration
 from hftlob.engine import book_process_, scan_through_entire_array_save_bidask
 from hftlob.layout import pack_lob_cfg
 from oracle import pyoracle as O
-from streams import init_book_messages, neg1_trade_streams, random_streams, top_streams
+from streams import full_book_messages, init_book_messages, neg1_trade_streams, noop_streams, random_streams, top_streams
 
 pytestmark = pytest.mark.gpu
 
@@ -125,5 +125,39 @@ def test_book_trade_row_neg1_fields(kw):
     a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
     msgs = neg1_trade_streams(E, M, seed=21 + cfg.nOrders)
     assert ((msgs[..., 4] == -1) & (msgs[..., 0] == 4)).any() and ((msgs[..., 6] == -1) & (msgs[..., 0] == 4)).any()
+    _run(cfg, msgs, a0, b0, empty_t)
+    _run(cfg, msgs, empty_a, empty_a, empty_t)
+
+
+def test_book_top_of_book_cache_4096():
+    """The top-of-book stress stream at the metric's size (4096 envs, 100 slots): the cached
+    top-of-book slot of each side against the oracle's formula on every crossing message."""
+    cfg = JAXLOB_Configuration()
+    E, M = 4096, 400
+    init = init_book_messages(E, seed=8)
+    empty_a = np.full((E, cfg.nOrders, 6), -1, np.int32)
+    empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
+    a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
+    _run(cfg, top_streams(E, M, seed=13), a0, b0, empty_t)
+
+
+NOOP_CASES = [dict(), dict(nOrders=16, nTrades=8), dict(nOrders=40, nTrades=30), dict(type_4_interpretation=1),
+              dict(cancel_mode=0), dict(cancel_mode=2), dict(nOrders=200, nTrades=150)]
+
+
+@pytest.mark.parametrize("kw", NOOP_CASES, ids=[str(k) or "default" for k in NOOP_CASES])
+def test_book_noop_skip(kw):
+    """The chunk pre-pass that skips messages leaving the book unchanged (streams.noop_streams:
+    unmatched cancels wrapping to the last slot, zero / -1 / negative quantities, doNothing rows,
+    init-id rows and adds, -1 fields) over books whose sides are 85-100 % full (the last slot
+    occupied or not, a few free rows) and over empty books: books, trades and every message's
+    best-quote record bit-exact."""
+    cfg = JAXLOB_Configuration(**kw)
+    E, M = 96, 320
+    empty_a = np.full((E, cfg.nOrders, 6), -1, np.int32)
+    empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
+    init = full_book_messages(E, seed=9, nO=cfg.nOrders)
+    a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
+    msgs = noop_streams(E, M, seed=31 + cfg.nOrders + 7 * cfg.cancel_mode, nO=cfg.nOrders)
     _run(cfg, msgs, a0, b0, empty_t)
     _run(cfg, msgs, empty_a, empty_a, empty_t)

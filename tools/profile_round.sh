@@ -4,7 +4,8 @@
 # (separate, per MI355X_MICROARCH.md).  Usage: [SLICES=G] tools/profile_round.sh TAG
 #   SLICES unset: the bench's default launch shape (MARLEnv.default_slices);
 #   0: the persistent k_env_rollout launch (the stats run uses 128 warm-up + 128 timed steps, so
-#      both launches are 128 steps long; the PMC runs one 32-step launch, warm-up 0);
+#      both launches are 128 steps long; the PMC runs one 128-step launch, warm-up 0, the same
+#      launch length, and the traffic passes also one 20-step launch: the driver's bench shape);
 #   G >= 1: k_env_step over G env slices (PMC runs: 4 warm-up + 32 steps, one step per launch).
 set -o pipefail
 T=${1:-r01}
@@ -13,7 +14,7 @@ mkdir -p $O
 cd $GRAFT_REPO_ROOT
 G=${SLICES:-0}  # the metric's default shape (MARLEnv.default_slices: the persistent launch at 4096 envs)
 if [ "$G" = 0 ]; then
-  KER=k_env_rollout; STATS_ARGS="--warmup 128 --steps 128"; PMC_ARGS="--warmup 0 --steps 32"; SPL=32; SSPL=128
+  KER=k_env_rollout; STATS_ARGS="--warmup 128 --steps 128"; PMC_ARGS="--warmup 0 --steps 128"; SPL=128; SSPL=128
 else
   KER=k_env_step; STATS_ARGS=""; PMC_ARGS="--warmup 4 --steps 32"; SPL=1; SSPL=1
 fi
@@ -26,6 +27,11 @@ B="python $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --slices $G"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- $B $STATS_ARGS > $O/stats_bench.json 2> $O/stats.err || exit 2
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $B $PMC_ARGS > $O/fetch.log 2>&1 || exit 3
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $B $PMC_ARGS > $O/write.log 2>&1 || exit 4
+if [ "$G" = 0 ]; then  # the driver's shape (bench.py --steps 20 --warmup 5): 20-step launches
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats20 -o run -- $B --warmup 20 --steps 20 > $O/stats20_bench.json 2> $O/stats20.err || exit 2
+  timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch20 -o run -- $B --warmup 0 --steps 20 > $O/fetch20.log 2>&1 || exit 3
+  timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write20 -o run -- $B --warmup 0 --steps 20 > $O/write20.log 2>&1 || exit 4
+fi
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_BRANCH --output-format csv -d $O/sq -o run -- $B $PMC_ARGS > $O/sq.log 2>&1 || exit 5
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY --output-format csv -d $O/lds -o run -- $B $PMC_ARGS > $O/lds.log 2>&1 || exit 6
 cd $GRAFT_REPO_ROOT

@@ -44,6 +44,14 @@ if stats:
             kstat = {"kernel_avg_us": round(float(r["AverageNs"]) / 1e3, 2), "launches": int(r["Calls"]),
                      "kernel_name": r["Name"], "steps_per_launch": STATS_SPL,
                      "kernel_us_per_step": round(float(r["AverageNs"]) / 1e3 / STATS_SPL, 3)}
+stats20 = glob.glob(os.path.join(d, "stats20", "**", "*kernel_stats.csv"), recursive=True)
+kstat20 = None
+for r in (csv.DictReader(open(stats20[0])) if stats20 else []):
+    if KERNEL in r["Name"]:  # two 20-step launches (--warmup 20 --steps 20): the driver's launch length
+        kstat20 = {"kernel_avg_us": round(float(r["AverageNs"]) / 1e3, 2), "launches": int(r["Calls"]),
+                   "steps_per_launch": 20, "kernel_us_per_step": round(float(r["AverageNs"]) / 1e3 / 20, 3)}
+        print("== rocprofv3 stats, 20-step launches:", kstat20)
+        break
 fetch_kb, write_kb = per_launch("fetch", "FETCH_SIZE"), per_launch("write", "WRITE_SIZE")
 bench = json.load(open(os.path.join(d, "stats_bench.json"))) if os.path.exists(os.path.join(d, "stats_bench.json")) else {}
 E = bench.get("config", {}).get("num_envs_per_gpu", 4096)
@@ -58,6 +66,11 @@ if fetch_kb is not None and write_kb is not None:
            "envs_per_launch": E // G, "steps_per_launch": SPL}
     json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
     print(f"== HBM traffic per {KERNEL} launch:", json.dumps(out))
+fetch20, write20 = per_launch("fetch20", "FETCH_SIZE"), per_launch("write20", "WRITE_SIZE")
+if out and fetch20 is not None and write20 is not None:  # the driver's shape: one 20-step launch
+    out["hbm_bytes_per_env_step_20_step_launch"] = round((2 * fetch20 + write20) * 1024 / E / 20, 1)
+    json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
+    print("== HBM traffic per env-step, one 20-step launch:", out["hbm_bytes_per_env_step_20_step_launch"])
 sq = {}
 for r in rows("sq"):
     if KERNEL in r["Kernel_Name"]:
@@ -84,13 +97,19 @@ if os.path.exists(sm) and os.path.getsize(sm):
 
 # one wave per env: per-wave counts / steps per launch are per env-step
 prof = dict(kstat or {})
+if kstat20:
+    prof["rocprof_20_step_launch"] = kstat20
 prof.update({"kernel": KERNEL, "slices": shape.get("slices", G), "envs_per_launch": E // G,
              "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d))})
 if "INSTS_SALU" in per_wave:
     prof["salu_per_env_step"] = per_wave["INSTS_SALU"]
     prof["valu_per_env_step"] = per_wave.get("INSTS_VALU")
     prof["wave_cycles_per_env_step"] = per_wave.get("WAVE_CYCLES")
-if out:
+if out:  # keyed by the launch length the traffic was counted on
     prof["hbm_bytes_per_env_step"] = out["hbm_bytes_per_env_step"]
+    prof["traffic_steps_per_launch"] = SPL
+    prof["hbm_bytes_per_env_step_by_launch_steps"] = {str(SPL): out["hbm_bytes_per_env_step"]}
+    if "hbm_bytes_per_env_step_20_step_launch" in out:
+        prof["hbm_bytes_per_env_step_by_launch_steps"]["20"] = out["hbm_bytes_per_env_step_20_step_launch"]
 json.dump(prof, open(os.path.join(d, "kernel_profile.json"), "w"), indent=1)
 print("== kernel_profile.json:", json.dumps(prof))
