@@ -2406,6 +2406,80 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     return o;
 }
 
+// Rollout steps' keys in batches (k_env_rollout; partitionable keys, <= 3 agents, <= 8 action
+// rows, <= 6 agent types, agents + action rows <= 10).  Speed_test's actions are random, so step t + j's keys depend only on
+// the master-key chain: up to KB_STEPS steps are derived at once, step j in lanes 16j..16j+15
+// (ll = lane & 15: the lanes of step_keys' two-lane layout, folded into 16: ll 0 / 1 / 2 + t the
+// first level, agent ag's two randint words in ll 8 + ag and 12 + ag, shuffle words in ll < A).
+// The master chain (split(m_j, n + 1)[0]) and the env keys (split(m_j, n + 1)[e + 1]) take one
+// level per step, then the four levels below the env key run for all the batch's steps at once:
+// 4 + 4 dependent threefry levels per 4 steps instead of 5 per step.  Bit-identical to step_keys.
+// Output per step j in LDS, kb[j * kb_words(c) + ...]: key (2), k1 (2), key_reset (2), the
+// agents' actions (n_agents), the shuffle words (A).
+#define KB_STEPS 4
+__host__ __device__ inline bool kb_ok(const hftlob_env_cfg& c) {  // (a step's row: one word per lane of its 16)
+    return c.prng_partitionable && c.n_agents <= 3 && c.n_action_msgs <= 8 && c.n_types <= 6 &&
+           6 + c.n_agents + c.n_action_msgs <= 16;
+}
+__host__ __device__ inline int kb_words(const hftlob_env_cfg& c) { return 6 + c.n_agents + c.n_action_msgs; }
+template <bool MD>
+DEV void step_keys_batch(const hftlob_env_cfg& c, int n_env, int e, Key& mk, int nb, i32* kb) {
+    const bool part = true;
+    const int l = lane_id(), ll = l & 15, j = l >> 4, nTy = c.n_types, A = c.n_action_msgs, KW = kb_words(c);
+    // the chain: level q gives m_{q+1} (lane 0) and step q's env key (lane 1)
+    i32 ka = 0, kb2 = 0;  // lane 16j: step j's env key
+#pragma unroll 1
+    for (int q = 0; q < nb; ++q) {
+        const Key v = split_key(mk, n_env + 1, l == 1 ? e + 1 : 0, part);
+        ka = wlane(ka, rdl((i32)v.a, 1), 16 * q);
+        kb2 = wlane(kb2, rdl((i32)v.b, 1), 16 * q);
+        mk = Key{(u32)rdl((i32)v.a, 0), (u32)rdl((i32)v.b, 0)};
+    }
+    const int b0 = l & ~15;  // this lane's step block
+    const Key key{(u32)__builtin_amdgcn_ds_bpermute(b0 << 2, ka), (u32)__builtin_amdgcn_ds_bpermute(b0 << 2, kb2)};
+    const bool hi_lane = ll >= 12;
+    const int ag = ll - (hi_lane ? 12 : 8);
+    int t = 0, i = 0;
+    agent_of_lane(c, ag < 0 ? 0 : ag, t, i);
+    const bool agent_lane = (ll >= 8) & (ag >= 0) & (ag < c.n_agents);
+    const Key L1 = split_key(key, ll < 2 ? 2 : nTy, ll < 2 ? ll : ll - 2, part);
+    const Key P2 = from_lane(L1, b0 + (agent_lane ? 2 + t : 0));
+    const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
+    const Key L3 = split_key(L2, 2, ((ll == 0) | hi_lane) ? 1 : 0, part);
+    const Key sub = from_lane(L3, b0);
+    const u32 bits = random_bits(ll < A ? sub : L3, 1, ll < A ? ll : 0, part);
+    const u32 hb = bits, lb = (u32)__builtin_amdgcn_ds_bpermute(((l + 4) & 63) << 2, (i32)bits);
+    const i32 na = agent_lane ? (MD ? action_hi(c.types[t]) : c.types[t].n_actions) : 1;
+    const u32 span = na <= 0 ? 1u : (u32)na;
+    u32 mult = 65536u % span;
+    mult = (mult * mult) % span;
+    const i32 act = (i32)(((hb % span) * mult + (lb % span)) % span);
+    // LDS: lane 16j + w writes word w of step j's row: 0..5 keys (from lanes ll 0 / 1 of L1 and
+    // the block's env key), 6 + ag the actions (ll 8 + ag), 6 + n_agents + r the shuffle words
+    // (ll 2 / 3: k1 = L1 of ll 0; ll 4 / 5: key_reset = L1 of ll 1)
+    const i32 l1a = __builtin_amdgcn_ds_bpermute((b0 + ((ll >> 2) & 1)) << 2, (i32)L1.a);
+    const i32 l1b = __builtin_amdgcn_ds_bpermute((b0 + ((ll >> 2) & 1)) << 2, (i32)L1.b);
+    const i32 ac = __builtin_amdgcn_ds_bpermute((b0 + 8 + (ll >= 6 ? ll - 6 : 0)) << 2, act);
+    const i32 sh = __builtin_amdgcn_ds_bpermute((b0 + (ll >= 6 + c.n_agents ? ll - 6 - c.n_agents : 0)) << 2, (i32)bits);
+    i32 w = ll == 0 ? (i32)key.a : (ll == 1 ? (i32)key.b : ((ll & 1) ? l1b : l1a));
+    w = ll >= 6 + c.n_agents ? sh : (ll >= 6 ? ac : w);
+    if ((j < nb) & (ll < KW)) kb[j * KW + ll] = w;
+    lds_order();
+}
+// step j's keys from the batch row (as step_keys would derive them)
+DEV StepKeys load_keys(const hftlob_env_cfg& c, const i32* row) {
+    const int l = lane_id(), na = c.n_agents, A = c.n_action_msgs;
+    StepKeys o;
+    o.key = Key{(u32)uni(row[0]), (u32)uni(row[1])};
+    o.k1 = Key{(u32)uni(row[2]), (u32)uni(row[3])};
+    o.key_reset = Key{(u32)uni(row[4]), (u32)uni(row[5])};
+    o.next_master = Key{0u, 0u};
+    const int ag = l - 32;
+    o.acts = (ag >= 0) & (ag < na) ? row[6 + (ag < 0 ? 0 : ag)] : 0;
+    o.shuffle_bits = l < A ? (u32)row[6 + na + (l < A ? l : 0)] : 0u;
+    return o;
+}
+
 // BaseLOBEnv.get_data_messages, fixed_time (base_env.py:358-367): a data row
 // whose time_s >= the episode end time becomes [0 x 6, time_s, time_ns]
 DEV void fixed_time_mask(int4& x, int4& y, i32 t_end) {
@@ -2481,7 +2555,8 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                       const i32* __restrict__ init_states, i32* __restrict__ state, float* __restrict__ obs_out,
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
                       i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
-                      i32* __restrict__ debug_out, i32* lds, bool resident, bool keep, u32& fl_carry) {
+                      i32* __restrict__ debug_out, i32* lds, bool resident, bool keep, u32& fl_carry,
+                      const i32* pre_keys = nullptr) {
     STAMP(t_start);
 #ifdef HFTLOB_STAMPS
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the in-kernel clock
@@ -2507,8 +2582,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const int naw = c.rec_words - c.off_agents;
     const bool agw_pre = naw <= 64;
     const i32 agw = (agw_pre & (l < naw)) ? rec[c.off_agents + l] : 0;
-    const StepKeys SK = step_keys<NFIX == 0>(c, key_n, ek, keys, master, mk);
-    if (master) mk = SK.next_master;
+    // (pre_keys: this step's row of a k_env_rollout key batch, step_keys_batch)
+    const StepKeys SK = pre_keys ? load_keys(c, pre_keys) : step_keys<NFIX == 0>(c, key_n, ek, keys, master, mk);
+    if (master && !pre_keys) mk = SK.next_master;
     const Key key_reset = SK.key_reset;
     if (RC) {  // the scan's key: k1, or split(k1)[0] after the shuffle split (marl_env.py:293-294,349-351)
         B.ek = c.shuffle_action_messages ? split_key(SK.k1, 2, 0, c.prng_partitionable) : SK.k1;
@@ -2987,15 +3063,22 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
     const unsigned long long wt_start = __builtin_amdgcn_s_memtime(), wt_rstart = __builtin_amdgcn_s_memrealtime();
     const u32 wt_hwid = __builtin_amdgcn_s_getreg(0xF804), wt_xcc = __builtin_amdgcn_s_getreg(0x7814);
 #endif
+    // the key batches (step_keys_batch) live after the book in LDS
+    const bool kbat = kb_ok(c);
+    const int kbw = kb_words(c);
+    i32* kbuf = lds + (c.n_cancel_msgs + c.n_action_msgs) * 8 + ((c.n_agents * 6 + 3) & ~3) +
+                12 * (NFIX > 0 ? NFIX : c.lob.n_orders) + 8 * (NFIX > 0 ? NFIX : c.lob.n_trades) + 256;
 #pragma unroll 1
     for (int t = 0; t < n_steps; ++t) {
         const size_t o = per_step ? (size_t)t * n_env : 0;
+        const int tb = t % KB_STEPS;
         kcfg_t* cp = kp;
         i32* st = state;
         const i32* md = msg_data;
         const i32* is = init_states;
         asm volatile("" : "+s"(cp), "+s"(st), "+s"(md), "+s"(is));
         const hftlob_env_cfg& cc = *(const hftlob_env_cfg*)cp;
+        if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
         const bool reset = env_step_dev<S, NFIX, RC>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
@@ -3003,7 +3086,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
             out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
             out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr,
             out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds, NFIX > 0 && resident,
-            NFIX > 0 && t + 1 < n_steps, fl);
+            NFIX > 0 && t + 1 < n_steps, fl, kbat ? kbuf + tb * kbw : nullptr);
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
 #ifndef HFTLOB_NO_BALANCE
         if (t + 1 < n_steps) balance_prio(bal_hwid, bal_xcc, bal_r0, t + 1, n_steps - t - 1);
@@ -3191,7 +3274,8 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
 #endif
 static size_t env_shm(const hftlob_env_cfg* cfg) {
     const size_t b = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
-                          12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4);
+                          12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4 +
+                          (kb_ok(*cfg) ? KB_STEPS * kb_words(*cfg) : 0));
     return b < (size_t)HFTLOB_LDS_FLOOR ? (size_t)HFTLOB_LDS_FLOOR : b;
 }
 

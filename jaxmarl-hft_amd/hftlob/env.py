@@ -438,10 +438,14 @@ class MARLEnv:
 
     def lds_bytes_per_env(self) -> int:
         """Dynamic LDS of one env's workgroup (env_shm in hftlob.hip): agent rows, action extras,
-        the two book sides, the trade log and the scratch row."""
+        the two book sides, the trade log, the pad / filter / scratch rows and the rollout's key
+        batches."""
         c = self.cfg_c
+        kb = (4 * (6 + c.n_agents + c.n_action_msgs)   # the rollout's key batches (step_keys_batch)
+              if c.prng_partitionable and c.n_agents <= 3 and c.n_action_msgs <= 8 and c.n_types <= 6
+              and 6 + c.n_agents + c.n_action_msgs <= 16 else 0)
         return 4 * ((c.n_cancel_msgs + c.n_action_msgs) * 8 + ((c.n_agents * 6 + 3) & ~3) +
-                    12 * c.lob.n_orders + 8 * c.lob.n_trades + 64 * 4)
+                    12 * c.lob.n_orders + 8 * c.lob.n_trades + 64 * 4 + kb)
 
     def resident_envs(self) -> int:
         """Envs of this config the GPU holds at once (workgroups per CU by LDS and by waves)."""
