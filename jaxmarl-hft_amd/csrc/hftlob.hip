@@ -341,7 +341,7 @@ template <int S>
 struct Side {
     i32* t;              // LDS table [6][R]
     i32* scr;            // LDS scratch row (64 words)
-    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid under F_OK
+    i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid unless F_STALE
     i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
                          // every handler reads prices, only adds and row clears write them
     // top-of-book cache: the slot _get_top_*_order_idx returns for max / min price top_p, and its
@@ -361,7 +361,8 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 
 // Wave-uniform book flags, one SGPR bitfield (bools would each be a 64-bit
 // lane mask the compiler copies at every merge):
-//   OK     the side's cached best quote is valid
+//   STALE  the side's cached best quote must be recomputed (one s_and tests both sides
+//          after a message)
 //   CLEAN  every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
 //          ever has to look at the row just written
 //   NEG1   some row with p != -1 holds a -1 in another field (then "first row
@@ -373,10 +374,10 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 // (bit 0 is left unused: a branch on a bit-0 test compiles to s_bitcmp1 + a 64-bit lane mask
 // + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc.  F_FAST,
 // tested once per message, is the sign bit: (i32)fl < 0 is one s_cmp_lt_i32)
-enum : u32 { F_OK_A = 2, F_OK_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64,
+enum : u32 { F_STALE_A = 2, F_STALE_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64,
              F_PM1_A = 256, F_PM1_B = 512, F_FAST = 0x80000000u };
 template <bool ASKS> struct SideBits {
-    static constexpr u32 OK = ASKS ? F_OK_A : F_OK_B;
+    static constexpr u32 STALE = ASKS ? F_STALE_A : F_STALE_B;
     static constexpr u32 CLEAN = ASKS ? F_CLEAN_A : F_CLEAN_B;
     static constexpr u32 NEG1 = ASKS ? F_NEG1_A : F_NEG1_B;
     static constexpr u32 PM1 = ASKS ? F_PM1_A : F_PM1_B;
@@ -485,7 +486,7 @@ template <bool ASKS, int S> DEV void rzn(Side<S>& s, u32& fl, int R, const Valid
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
     clear_masked(s, R, m);
-    fl = (fl | SideBits<ASKS>::CLEAN) & ~SideBits<ASKS>::OK;
+    fl = fl | SideBits<ASKS>::CLEAN | SideBits<ASKS>::STALE;
     fl = (fl & ~F_FAST) | fast_bit(fl);
 }
 
@@ -515,13 +516,13 @@ DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i3
     bp = pa;
     bq = wave_sum(v);
 }
-// recompute a side's cached best quote (sets its OK bit)
+// recompute a side's cached best quote (clears its STALE bit)
 template <bool ASKS, int S> DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint) {
     i32 q[S];
     ldcol(s.t, R, FQ, q);
     if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q);
     else best_bid_pq(s.pc, q, V, s.best_p, s.best_q);
-    fl |= SideBits<ASKS>::OK;
+    fl &= ~SideBits<ASKS>::STALE;
 }
 
 // _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
@@ -667,17 +668,17 @@ DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i3
     // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
     // common case, an order behind the best (one compare each); per side the cases are those of
     // get_best_* with -1 (and, for asks, maxint) standing for "no price".
-    constexpr u32 OK = SideBits<!BID>::OK;
-    if (!(fl & OK)) { s.top = -1; return; }
+    constexpr u32 STALE = SideBits<!BID>::STALE;
+    if (fl & STALE) { s.top = -1; return; }
     const i32 bp = s.best_p;
     if (BID) {
         if (np < bp) {
-            if (bp == -1) fl &= ~OK;        // np < -1 on an empty side
+            if (bp == -1) fl |= STALE;        // np < -1 on an empty side
         } else if (np > bp) {
             s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
             top_new(s, e, np, t, tns, maxint);
         } else if (bp == -1) {
-            fl &= ~OK;                      // np == -1 on an empty side
+            fl |= STALE;                      // np == -1 on an empty side
         } else {
             s.best_q = wadd(s.best_q, nq);
             top_eq(s, e, t, tns, maxint);
@@ -685,13 +686,13 @@ DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i3
     } else {
         if (np > bp) {
             if (bp == -1) {                 // empty side
-                if (np == maxint) fl &= ~OK;
+                if (np == maxint) fl |= STALE;
                 else { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
             }
         } else if (np < bp) {
             if (np != -1) { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
         } else if (np == -1) {
-            fl &= ~OK;
+            fl |= STALE;
         } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
             top_eq(s, e, t, tns, maxint);
@@ -700,22 +701,22 @@ DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i3
 }
 // a row at price op lost dq of its quantity (possibly all of it)
 template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i32 dq) {
-    constexpr u32 OK = SideBits<ASKS>::OK;
-    if (!(fl & OK)) return;
+    constexpr u32 STALE = SideBits<ASKS>::STALE;
+    if (fl & STALE) return;
     if (op == s.best_p) {
         if (op == -1) {
-            fl &= ~OK;
+            fl |= STALE;
         } else {
             s.best_q = wsub(s.best_q, dq);
-            if (s.best_q <= 0) fl &= ~OK;  // level exhausted (or odd data): rescan
+            if (s.best_q <= 0) fl |= STALE;  // level exhausted (or odd data): rescan
         }
     } else {
         // a row behind the best: the quote stands unless a -1 price is involved (scalar selects;
         // as one branch on "op == -1 || best == -1" the compiler builds 64-bit lane masks)
         asm volatile("");
         u32 f = fl;
-        f = fresh(op) == -1 ? f & ~OK : f;
-        f = fresh(s.best_p) == -1 ? f & ~OK : f;
+        f = fresh(op) == -1 ? f | STALE : f;
+        f = fresh(s.best_p) == -1 ? f | STALE : f;
         fl = f;
     }
 }
@@ -786,14 +787,14 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
     // does not cross (the loop's own first test, with an empty ask side standing for maxint)
     // (fresh: the RARE / common handler copies each keep their own test, not one shared lane mask)
     if (fresh(qtm) <= 0) return qtm;
-    if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+    if (B.fl & SideBits<!BID>::STALE) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
     {
         const i32 bp = s.best_p;
         const i32 mp0 = (!BID && bp == -1) ? B.c.maxint : bp;
         if (__builtin_expect(BID ? mp0 < price : mp0 > price, 1)) return qtm;
     }
     while (qtm > 0) {
-        if (!(B.fl & SideBits<!BID>::OK)) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+        if (B.fl & SideBits<!BID>::STALE) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
         // the side's best; an empty ask side (-1) counts as maxint (_get_top_ask_order_idx).
         // BID: `s` is the bid side (an incoming sell crosses when best bid >= price)
         i32 mp = s.best_p;
@@ -840,7 +841,7 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
 template <bool BID, bool G, int S>
 DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
-    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, OK = SideBits<!BID>::OK,
+    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, STALE = SideBits<!BID>::STALE,
                   PM1 = SideBits<!BID>::PM1;
     const i32 nq = imax_(0, qty);
     if (!G) {  // FAST: "any -1" <=> p == -1 <=> an all -1 row; no free slot -> the last slot, which holds an order
@@ -850,10 +851,10 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
             if (m.h & (H_NEG1 | H_PM1)) B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
             if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
-            else { B.fl &= ~OK; s.top = -1; }
+            else { B.fl |= STALE; s.top = -1; }
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
             side_clr(s, R, e);
-            B.fl &= ~OK;
+            B.fl |= STALE;
         }
         return;
     }
@@ -886,10 +887,10 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         if (m.h & H_NEG1) B.fl |= NEG1;
         if (m.h & H_PM1) B.fl |= PM1;
         if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
-        else { B.fl &= ~OK; s.top = -1; }
+        else { B.fl |= STALE; s.top = -1; }
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         side_clr(s, R, e);
-        B.fl &= ~OK;
+        B.fl |= STALE;
     }
 }
 
@@ -914,7 +915,7 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
     // only the worst level goes: the best quote and the top of book survive unless the side holds
     // one price level (worst == best; an ask side whose prices are all maxint has best -1)
     s.top = worst != s.top_p ? top : -1;
-    if ((worst == s.best_p) | (s.best_p == -1)) B.fl &= ~SideBits<!BID>::OK;
+    if ((worst == s.best_p) | (s.best_p == -1)) B.fl |= SideBits<!BID>::STALE;
     free_slots(B, s, free);
 }
 // The common add: FAST book, a free (all -1) slot exists, no eviction: the order goes to the
@@ -1131,9 +1132,9 @@ DEV i32 ffill(i32 v, i32 carry) {
     return src < 0 ? carry : got;
 }
 template <int S> DEV void refresh_best(Book<S>& B) {
-    if ((B.fl & (F_OK_A | F_OK_B)) != (F_OK_A | F_OK_B)) {
-        if (!(B.fl & F_OK_A)) rescan<true>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint);
-        if (!(B.fl & F_OK_B)) rescan<false>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint);
+    if (B.fl & (F_STALE_A | F_STALE_B)) {
+        if (B.fl & F_STALE_A) rescan<true>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint);
+        if (B.fl & F_STALE_B) rescan<false>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint);
     }
 }
 
@@ -1249,7 +1250,7 @@ DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, 
             if (RC) B.mi = base + (int)k;
             process_msg<RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
             refresh_best(B);
-            const u32 kn = ff1(todo) & 63u;
+            const u32 kn = ff1(todo);  // (-1 once todo is empty: v_readlane takes the lane's low 6 bits)
             h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
             d4 = rdl(y.x, kn); d5 = rdl(y.y, kn); d6 = rdl(y.z, kn); d7 = rdl(y.w, kn);
             rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
@@ -1306,7 +1307,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     i32* ga = asks + (size_t)e * R * 6;
     i32* gb = bids + (size_t)e * R * 6;
     i32* gt = trades + (size_t)e * B.c.nT * 8;
-    B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs);
+    B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs) | F_STALE_A | F_STALE_B;
     B.fl |= fast_bit(B.fl);
     load_trades(B.tr, gt, B.vt);
     {  // the loaded log's free-row prefix (see Book::ntr)
@@ -2628,9 +2629,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     if (resident) {  // the book flags as the previous step left them (the cached best quotes are not kept)
         relink_side(B.a, R, B.vs);
         relink_side(B.b, R, B.vs);
-        B.fl = fl_carry & ~(u32)(F_OK_A | F_OK_B);
+        B.fl = fl_carry | F_STALE_A | F_STALE_B;
     } else {
-        B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs);
+        B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs) | F_STALE_A | F_STALE_B;
         B.fl |= fast_bit(B.fl);
     }
     STAMP(t_load);
