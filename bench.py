@@ -47,7 +47,7 @@ CONFIG = "2_player_fq_fqc"
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_CU, CLOCK_HZ = 256, 2.4e9    # MI355X CUs, max engine clock (MI355X_MICROARCH.md)
 CPU_STEPS = 64                 # CPU baseline / parity: one full episode (incl. the auto-reset)
-PROFILE = "r02_kernel_profile.json"  # profiles/: rocprof figures of the metric kernel (tools/profile_round.sh)
+PROFILE = "r03_kernel_profile.json"  # profiles/: rocprof figures of the metric kernel (tools/profile_round.sh)
 
 
 def parse_args(argv=None):
