@@ -223,10 +223,19 @@ def cpu_baseline(env, day, state0, master0, n_threads):
     t0 = time.perf_counter()
     st1, _ = O.rollout_sampled(c, m0, msgs, init, st0, CPU_STEPS, L=L)
     v1 = E * CPU_STEPS / (time.perf_counter() - t0)
+    _, facts = cpu_share()
+    aff = facts["affinity_cores"]
+    v_aff = None
+    if aff > thr:  # every core the affinity set shows (beyond the job's quota the threads time-slice)
+        L.oracle_set_threads(aff)
+        t0 = time.perf_counter()
+        st_aff, _ = O.rollout_sampled(c, m0, msgs, init, st0, CPU_STEPS, L=L)
+        v_aff = E * CPU_STEPS / (time.perf_counter() - t0)
+        if not (st_aff == st).all():
+            raise AssertionError("cpu_baseline: the all-affinity-cores and quota-thread CPU rollouts differ")
     L.oracle_set_threads(thr)
     if not (st1 == st).all():
         raise AssertionError("cpu_baseline: 1-thread and multi-thread CPU rollouts differ")
-    _, facts = cpu_share()
     eff = v / (thr * v1) if thr and v1 else None
     return {"value": round(v, 1), "unit": "env steps/s", "cores": thr, "kind": "port",
             "sample": (f"{E} envs x {CPU_STEPS} steps (one episode incl. auto-reset) of the metric config/day/seeds, "
@@ -234,6 +243,10 @@ def cpu_baseline(env, day, state0, master0, n_threads):
                        f"gcc -O3 -march=native, OpenMP {thr} threads"),
             "single_core_value": round(v1, 1), "single_core_sample": f"the same {E} x {CPU_STEPS} workload, 1 thread",
             "thread_scaling_efficiency": round(eff, 3) if eff else None,
+            "all_affinity_cores_value": round(v_aff, 1) if v_aff else None,
+            "all_affinity_cores_sample": (f"the same {E} x {CPU_STEPS} workload on {aff} OpenMP threads (every core "
+                                          "of the affinity set; the job's cgroup quota caps the CPU time)")
+            if v_aff else None,
             "cores_rule": ("threads = this job's host CPU share: the affinity set capped by the cgroup quota and "
                            "OMP_NUM_THREADS (bench.py cpu_share)"),
             "cpu_model": model, "nproc": os.cpu_count(), **facts}, st
