@@ -456,14 +456,20 @@ class MARLEnv:
 
     def default_slices(self, n_env: int) -> int:
         """Launch shape of rollout_sampled, measured on 1x MI355X (DESIGN.md section 4,
-        tools/sweep_envs.sh, tools/gpu_sweep.sh): 0 = one persistent launch (every env's steps back
-        to back, its book kept in LDS) while the whole batch is resident (the metric config: 16
-        envs per CU, 4096 envs; 512 / 2048 / 4096 envs: 9.9 / 33.5 / 49.6 M env-steps/s against
-        7.7 / 28.3 / 47.5 M for 2 slices); otherwise 2 env slices on their own streams (8192 /
-        16384 envs: 57.2 / 58.9 M against 53.0 / 56.5 M persistent, whose later workgroups wait for
-        whole rollouts of the first; Speed_test's [5,5] / [10,10] agents at 4000 envs, whose agent
-        rows leave room for 14 / 11 envs per CU: 24.1 / 14.7 M against 19.4 / 11.4 M)."""
-        return 0 if n_env <= self.resident_envs() else 2
+        tools/sweep_envs.sh, tools/gpu_sweep.sh; profiles/r03_launch_shape_sweep.txt): 0 = one
+        persistent launch (every env's steps back to back, its book kept in LDS, issue priority by
+        projected finish) whenever its waves of workgroups are full: the whole batch resident, or
+        whole multiples of what the GPU holds at once (the metric config, 16 envs per CU:
+        512 / 2048 / 4096 / 8192 / 16384 envs at 10.2 / 37.4 / 62.3 / 64.0 / 64.7 M env-steps/s
+        against 7.7 / 28.6 / 47.8 / 59.7 / 61.6 M for 2 slices); 2 env slices on their own streams
+        when the last wave would be partly empty, as its envs would run whole rollouts after the
+        others finish (Speed_test's [5,5] / [10,10] agents at 4000 envs, whose agent rows leave
+        room for 14 / 11 envs per CU: 25.1 / 15.7 M against 19.7 / 12.3 M)."""
+        cap = self.resident_envs()
+        if n_env <= cap:
+            return 0
+        waves = -(-n_env // cap)
+        return 0 if n_env >= 0.9 * waves * cap else 2
 
     def prepare_rollout(self, n_slices: int) -> None:
         """Create the library's slice streams for `n_slices` on this env's device (host-only).

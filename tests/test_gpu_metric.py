@@ -80,14 +80,16 @@ def test_rollout_shards_equal_whole_batch():
 
 
 def test_default_launch_shape():
-    """MARLEnv.default_slices: the persistent launch while the whole batch is resident (the
-    metric: 4096 envs at 16 per CU), 2 env slices beyond, and for configs whose agent rows leave
-    fewer envs per CU (Speed_test's [5, 5] agents at 4000 envs; profiles/r02_*sweep*)."""
+    """MARLEnv.default_slices: the persistent launch while its waves of workgroups are full (the
+    metric: 4096 envs at 16 per CU, and whole multiples of it), 2 env slices when the last wave
+    would be partly empty (Speed_test's [5, 5] agents at 4000 envs, 14 envs per CU;
+    profiles/r03_launch_shape_sweep.txt, r03_speed_test_sweep.json)."""
     cfg = builtin_config("2_player_fq_fqc")
     env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
     assert env.lds_bytes_per_env() * 16 <= env.LDS_PER_CU
     assert env.default_slices(4096) == 0 and env.default_slices(512) == 0
-    assert env.default_slices(8192) == 2
+    assert env.default_slices(8192) == 0 and env.default_slices(16384) == 0
+    assert env.default_slices(6000) == 2
     big = dataclasses.replace(builtin_config("default"), number_of_agents_per_type=[5, 5])
     env5 = MARLEnv(None, big, data=_day(big.world_config, 2_000_000))
     assert env5.default_slices(4000) == 2
