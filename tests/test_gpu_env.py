@@ -577,3 +577,45 @@ def test_reference_env_config_runs(fname):
     from hftlob.config_io import dict_to_multiagent_config
     cfg = dict_to_multiagent_config(_ref_configs()[fname])
     rollout_parity(cfg, E=16, K=24)
+
+
+def test_concurrent_persistent_rollouts():
+    """Two persistent rollouts on two streams at once (their waves share SIMDs and the kernel's
+    issue-priority table, k_env_rollout's balance_prio), and a batch larger than the GPU holds at
+    once (later workgroups reuse the hardware wave slots of finished ones): each equals the same
+    rollout run alone, bit for bit.  The priority rule orders issue, never results."""
+    cfg = builtin_config("2_player_fq_fqc")
+    env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
+    params = env.default_params
+    T = 70  # crosses the auto-reset
+    runs = []
+    for E, seed in ((3000, 1), (2000, 2), (9000, 3)):
+        keys = torch.from_numpy((np.arange(2 * E, dtype=np.uint32).reshape(E, 2) + 7 * seed).view(np.int32)).cuda()
+        _, s = env.reset(keys, params)
+        runs.append((E, s, torch.tensor([seed, 5], dtype=torch.int32, device="cuda")))
+    ref = []
+    for E, s, k0 in runs:  # alone
+        s1 = s.clone(env)
+        kout = torch.empty(2, dtype=torch.int32, device="cuda")
+        env.rollout_sampled(k0.clone(), kout, s1, params, T, n_slices=0)
+        torch.cuda.synchronize()
+        ref.append((s1.buf.clone(), kout.clone()))
+    streams = [torch.cuda.Stream() for _ in runs[:2]]
+    outs = []
+    for (E, s, k0), st in zip(runs[:2], streams):  # the first two concurrently
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            s2 = s.clone(env)
+            kout = torch.empty(2, dtype=torch.int32, device="cuda")
+            env.rollout_sampled(k0.clone(), kout, s2, params, T, n_slices=0)
+            outs.append((s2, kout))
+    torch.cuda.synchronize()
+    for (s2, kout), (rs, rk) in zip(outs, ref[:2]):
+        assert (s2.buf == rs).all() and (kout == rk).all()
+    # the over-full batch, again alone: the same as its first run (no dependence on slot reuse)
+    E, s, k0 = runs[2]
+    s3 = s.clone(env)
+    kout = torch.empty(2, dtype=torch.int32, device="cuda")
+    env.rollout_sampled(k0.clone(), kout, s3, params, T, n_slices=0)
+    torch.cuda.synchronize()
+    assert (s3.buf == ref[2][0]).all() and (kout == ref[2][1]).all()
