@@ -2332,12 +2332,31 @@ struct StepKeys {
     i32 acts;          // lane 32 + ag: sampled action (rollout mode)
 };
 // agent lane 32 + ag -> (type, index within type)
+// (per-lane type fields: each type's field is a uniform (scalar) load and the lane selects by its
+// t; indexing c.types[t] with a lane-varying t would be a vector load from the kernel arguments,
+// waited on at once, per use)
+// (sel: a select of the loaded VALUES; as a plain ?: the compiler selects the field's address
+// per lane and issues the vector load anyway)
+DEV i32 type_n_agents(const hftlob_env_cfg& c, int t) {
+    i32 v = c.types[0].n_agents;
+#pragma unroll
+    for (int k = 1; k < HFTLOB_MAX_TYPES; ++k) v = sel(t == k, c.types[k].n_agents, v);
+    return v;
+}
+DEV i32 type_action_hi(const hftlob_env_cfg& c, int t, bool md) {
+    i32 v = md ? action_hi(c.types[0]) : c.types[0].n_actions;
+#pragma unroll
+    for (int k = 1; k < HFTLOB_MAX_TYPES; ++k) v = sel(t == k, md ? action_hi(c.types[k]) : c.types[k].n_actions, v);
+    return v;
+}
 DEV void agent_of_lane(const hftlob_env_cfg& c, int ag, int& t, int& i) {
     t = 0;
     i = ag;
 #pragma unroll
-    for (int k = 0; k < HFTLOB_MAX_TYPES - 1; ++k)
-        if (k < c.n_types - 1 && i >= c.types[t].n_agents) { i -= c.types[t].n_agents; ++t; }
+    for (int k = 0; k < HFTLOB_MAX_TYPES - 1; ++k) {
+        const i32 nk = c.types[k].n_agents;  // (t == k while every earlier test held)
+        if ((k < c.n_types - 1) & (t == k) & (i >= nk)) { i -= nk; ++t; }
+    }
 }
 DEV Key lane_key(Key v) { return Key{(u32)rdl((i32)v.a, 0), (u32)rdl((i32)v.b, 0)}; }
 DEV Key from_lane(Key v, int src) {  // per-lane gather v[src]
@@ -2374,7 +2393,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     o.key_reset = Key{(u32)rdl((i32)L1.a, 1), (u32)rdl((i32)L1.b, 1)};
     if (two) {
         const Key P2 = from_lane(L1, agent_lane ? 2 + t : 0);
-        const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
+        const Key L2 = split_key(P2, agent_lane ? type_n_agents(c, t) : 2, agent_lane ? i : 1, part);
         // L3: lane 0 sub = split(sk)[1]; lane 32 + ag split(k_ag)[0]; lane 48 + ag split(k_ag)[1]
         const Key L3 = split_key(L2, 2, ((l == 0) | hi_lane) ? 1 : 0, part);
         // L4: lanes < A random_bits(sub, A)[l]; agent lanes random_bits(their key, 1)[0]
@@ -2382,7 +2401,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
         const u32 bits = random_bits(l < A ? sub : L3, 1, l < A ? l : 0, part);
         o.shuffle_bits = bits;
         const u32 hb = bits, lb = (u32)__builtin_amdgcn_ds_bpermute(((l + 16) & 63) << 2, (i32)bits);
-        const i32 na = agent_lane ? (MD ? action_hi(c.types[t]) : c.types[t].n_actions) : 1;
+        const i32 na = agent_lane ? type_action_hi(c, t, MD) : 1;
         const u32 span = na <= 0 ? 1u : (u32)na;
         u32 mult = 65536u % span;
         mult = (mult * mult) % span;
@@ -2391,7 +2410,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     }
     // L2: lane 0 sk = split(k1)[1]; agent lanes: split(sub_t, n_agents_t)[i]
     const Key P2 = from_lane(L1, agent_lane ? 2 + t : 0);
-    const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
+    const Key L2 = split_key(P2, agent_lane ? type_n_agents(c, t) : 2, agent_lane ? i : 1, part);
     // L3: lane 0 sub = split(sk)[1]; agent lanes: randint's two keys
     const Key L3a = split_key(L2, 2, l == 0 ? 1 : 0, part);
     const Key L3b = split_key(L2, 2, 1, part);
@@ -2399,7 +2418,7 @@ DEV StepKeys step_keys(const hftlob_env_cfg& c, int n_env, int e, const u32* key
     const Key sub = from_lane(L3a, 0);
     o.shuffle_bits = random_bits(sub, A > 0 ? A : 1, l < A ? l : 0, part);
     const u32 hb = random_bits(L3a, 1, 0, part), lb = random_bits(L3b, 1, 0, part);
-    const i32 na = agent_lane ? (MD ? action_hi(c.types[t]) : c.types[t].n_actions) : 1;
+    const i32 na = agent_lane ? type_action_hi(c, t, MD) : 1;
     const u32 span = na <= 0 ? 1u : (u32)na;  // randint(key, 0, n_actions)
     u32 mult = 65536u % span;
     mult = (mult * mult) % span;
@@ -2445,12 +2464,12 @@ DEV void step_keys_batch(const hftlob_env_cfg& c, int n_env, int e, Key& mk, int
     const bool agent_lane = (ll >= 8) & (ag >= 0) & (ag < c.n_agents);
     const Key L1 = split_key(key, ll < 2 ? 2 : nTy, ll < 2 ? ll : ll - 2, part);
     const Key P2 = from_lane(L1, b0 + (agent_lane ? 2 + t : 0));
-    const Key L2 = split_key(P2, agent_lane ? c.types[t].n_agents : 2, agent_lane ? i : 1, part);
+    const Key L2 = split_key(P2, agent_lane ? type_n_agents(c, t) : 2, agent_lane ? i : 1, part);
     const Key L3 = split_key(L2, 2, ((ll == 0) | hi_lane) ? 1 : 0, part);
     const Key sub = from_lane(L3, b0);
     const u32 bits = random_bits(ll < A ? sub : L3, 1, ll < A ? ll : 0, part);
     const u32 hb = bits, lb = (u32)__builtin_amdgcn_ds_bpermute(((l + 4) & 63) << 2, (i32)bits);
-    const i32 na = agent_lane ? (MD ? action_hi(c.types[t]) : c.types[t].n_actions) : 1;
+    const i32 na = agent_lane ? type_action_hi(c, t, MD) : 1;
     const u32 span = na <= 0 ? 1u : (u32)na;
     u32 mult = 65536u % span;
     mult = (mult * mult) % span;
