@@ -424,7 +424,8 @@ def main(argv=None):
             a = prof["salu_per_env_step"] * world * E * args.steps / elapsed / N_CU / world
             issue = {"bound": "salu_issue", "achieved": round(a / 1e9, 4), "peak": CLOCK_HZ / 1e9,
                      "unit": "G SALU instr/s per CU", "frac": round(a / CLOCK_HZ, 4),
-                     "salu_per_env_step": prof["salu_per_env_step"], "source": prof.get("source")}
+                     "salu_per_env_step": prof["salu_per_env_step"], "source": prof.get("source"),
+                     "salu_steps_per_launch": prof.get("traffic_steps_per_launch", prof.get("steps_per_launch"))}
     workload = (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, {env.num_msgs_per_step} msgs/step, "
                 "auto-reset, Speed_test semantics" if metric_cfg else
                 f"{args.config if args.config == 'default' else args.config + '.json'} "
