@@ -420,7 +420,12 @@ def main(argv=None):
     if prof:
         roofline["rocprof"] = rp
         if prof.get("salu_per_env_step"):
-            # the CU's one scalar ALU, shared by its waves, is the scarcest pipe
+            # the CU's one scalar ALU, shared by its waves, is the scarcest pipe;
+            # SALU per env-step from the SQ pass over the launch length nearest this run's
+            sby = prof.get("salu_per_env_step_by_launch_steps") or {
+                str(prof.get("traffic_steps_per_launch", prof.get("steps_per_launch", T))): prof["salu_per_env_step"]}
+            s_spl = min(sby, key=lambda k: abs(int(k) - T))
+            prof = dict(prof, salu_per_env_step=sby[s_spl], traffic_steps_per_launch=int(s_spl))
             a = prof["salu_per_env_step"] * world * E * args.steps / elapsed / N_CU / world
             issue = {"bound": "salu_issue", "achieved": round(a / 1e9, 4), "peak": CLOCK_HZ / 1e9,
                      "unit": "G SALU instr/s per CU", "frac": round(a / CLOCK_HZ, 4),

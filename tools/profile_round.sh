@@ -31,6 +31,7 @@ if [ "$G" = 0 ]; then  # the driver's shape (bench.py --steps 20 --warmup 5): 20
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats20 -o run -- $B --warmup 20 --steps 20 > $O/stats20_bench.json 2> $O/stats20.err || exit 2
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/fetch20 -o run -- $B --warmup 0 --steps 20 > $O/fetch20.log 2>&1 || exit 3
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/write20 -o run -- $B --warmup 0 --steps 20 > $O/write20.log 2>&1 || exit 4
+  timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_BRANCH --output-format csv -d $O/sq20 -o run -- $B --warmup 0 --steps 20 > $O/sq20.log 2>&1 || exit 5
 fi
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_BRANCH --output-format csv -d $O/sq -o run -- $B $PMC_ARGS > $O/sq.log 2>&1 || exit 5
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY --output-format csv -d $O/lds -o run -- $B $PMC_ARGS > $O/lds.log 2>&1 || exit 6

@@ -81,6 +81,16 @@ if sq:
     per_wave = {k.replace("SQ_", ""): round(sum(v) / len(v) / w / SPL, 1) for k, v in sorted(sq.items())
                 if k != "SQ_WAVES"}
     print(f"== SQ counters per wave and env-step ({KERNEL}):", per_wave)
+sq20 = {}
+for r in rows("sq20"):  # the driver's launch length: one 20-step launch
+    if KERNEL in r["Kernel_Name"]:
+        sq20.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+per_wave20 = {}
+if sq20:
+    w = sum(sq20["SQ_WAVES"]) / len(sq20["SQ_WAVES"])
+    per_wave20 = {k.replace("SQ_", ""): round(sum(v) / len(v) / w / 20, 1) for k, v in sorted(sq20.items())
+                  if k != "SQ_WAVES"}
+    print(f"== SQ counters per wave and env-step, one 20-step launch ({KERNEL}):", per_wave20)
 lds = {}
 for r in rows("lds"):
     if KERNEL in r["Kernel_Name"]:
@@ -101,6 +111,8 @@ if kstat20:
     prof["rocprof_20_step_launch"] = kstat20
 prof.update({"kernel": KERNEL, "slices": shape.get("slices", G), "envs_per_launch": E // G,
              "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d))})
+if "INSTS_SALU" in per_wave20:
+    prof["salu_per_env_step_by_launch_steps"] = {str(SPL): per_wave.get("INSTS_SALU"), "20": per_wave20["INSTS_SALU"]}
 if "INSTS_SALU" in per_wave:
     prof["salu_per_env_step"] = per_wave["INSTS_SALU"]
     prof["valu_per_env_step"] = per_wave.get("INSTS_VALU")
