@@ -47,7 +47,7 @@ CONFIG = "2_player_fq_fqc"
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 N_CU, CLOCK_HZ = 256, 2.4e9    # MI355X CUs, max engine clock (MI355X_MICROARCH.md)
 CPU_STEPS = 64                 # CPU baseline / parity: one full episode (incl. the auto-reset)
-PROFILE = "r03_kernel_profile.json"  # profiles/: rocprof figures of the metric kernel (tools/profile_round.sh)
+PROFILE = "r*_kernel_profile.json"  # profiles/: rocprof figures of the metric kernel (tools/profile_round.sh), newest round
 
 
 def parse_args(argv=None):
@@ -172,12 +172,30 @@ def cpu_share():
     return thr, {"affinity_cores": aff, "cgroup_quota_cores": quota, "omp_num_threads": omp}
 
 
-def _profile(name):
-    p = os.path.join(ROOT, "profiles", name)
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f)
-    return None
+def _profile(pattern):
+    """The newest round's profile summary (profiles/rNN_kernel_profile.json), with its file name."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not found:
+        return None
+    with open(found[-1]) as f:
+        return dict(json.load(f), file=os.path.join("profiles", os.path.basename(found[-1])))
+
+
+def timed_window(K: int, max_steps: int, ctr0: int = 0) -> str:
+    """Which steps of each env's episode the K timed steps cover: Speed_test's timed rollout starts
+    from the reset state (step counter 0), and an env's episode ends on the step whose counter
+    satisfies max_steps - step - 1 <= 1 (marl_env.py:711-718 _episode_done_time, then the auto-reset :787-803)."""
+    ends, ctr = [], ctr0
+    for t in range(K):
+        if max_steps - ctr - 1 <= 1:
+            ends.append(t)
+            ctr = 0
+        else:
+            ctr += 1
+    what = (f"{len(ends)} episode end(s) with auto-reset, at timed step(s) {ends}" if ends
+            else "no episode end (the auto-reset and the episode-end trades are outside the window)")
+    return f"timed steps 0-{K - 1} from the reset state (step counter {ctr0}), {max_steps}-step episodes: {what}"
 
 
 def compare_states(env, cpu, gpu) -> str:
@@ -319,6 +337,8 @@ def main(argv=None):
     master0 = all_keys[0].clone()
     _, state = env.reset(D.rank_keys(all_keys, rank, E).contiguous(), params)
     state0 = state.buf.clone()
+    max_steps = int(state.world_state.max_steps_in_episode[0].item())
+    ctr0 = int(state.world_state.step_counter[0].item())
     key_e0, key_n = rank * E, world * E
     if args.slices < 0:
         args.slices = env.default_slices(E)
@@ -404,18 +424,23 @@ def main(argv=None):
         r20 = prof.get("rocprof_20_step_launch")
         if r20 and abs(T - 20) < abs(T - rp.get("steps_per_launch", T)):
             rp = dict(rp, **r20)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+    # "hbm" is the normative roofline: the reference's per-step state I/O priced at
+    # the HBM peak.  The kernel does not run against it (limiter: issue and dependent latency)
+    roofline = {"bound": "hbm", "bound_kind": "normative: algorithmic bytes at HBM peak, not the limiter",
+                "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                 "kernel": kernel, "kernel_ms": round(kern_ms, 5), "bytes_per_env_step": per_env,
                 "units_per_launch": E,
                 "launches_per_step": (args.slices or round(1 / T, 6)) if args.mode == "rollout" else 3,
-                "limiter": ("issue / dependent latency, not HBM: the measured traffic is far below the algorithmic "
-                            "bytes (the books stay in LDS) and below the peak (measured_frac); see issue_roofline "
-                            "and DESIGN.md section 4")}
+                "limiter": ("issue / dependent latency, not HBM: the counted traffic is far below the algorithmic "
+                            "bytes (the books stay in LDS) and below the peak (counted_traffic_frac); see "
+                            "issue_roofline and DESIGN.md section 4")}
     if traffic is not None:
         roofline["traffic_steps_per_launch"] = t_spl
-        # the bandwidth the kernel really draws: counted HBM bytes per batched step / time per step
-        roofline["measured_frac"] = round(traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)
+        roofline["traffic_source"] = {"file": prof.get("file"), "run": prof.get("source"),
+                                      "commit": prof.get("commit")}
+        if t_spl == T:  # the counted HBM bytes of a launch of this run's length / this run's time per step
+            roofline["counted_traffic_frac"] = round(traffic / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)
     issue = None
     if prof:
         roofline["rocprof"] = rp
@@ -432,10 +457,10 @@ def main(argv=None):
                      "salu_per_env_step": prof["salu_per_env_step"], "source": prof.get("source"),
                      "salu_steps_per_launch": prof.get("traffic_steps_per_launch", prof.get("steps_per_launch"))}
     workload = (f"{CONFIG}.json MM fixed_quants + EXE fixed_quants_complex, {env.num_msgs_per_step} msgs/step, "
-                "auto-reset, Speed_test semantics" if metric_cfg else
+                "Speed_test semantics (auto-reset on)" if metric_cfg else
                 f"{args.config if args.config == 'default' else args.config + '.json'} "
                 f"agents {list(cfg.number_of_agents_per_type)}, {env.num_msgs_per_step} msgs/step, "
-                "auto-reset, Speed_test semantics")
+                "Speed_test semantics (auto-reset on)")
     line = {
         "metric": "env steps/sec (whole node), 2-agent MARL, 10-level LOB, NUM_ENVS=4096",
         "value": round(value, 1),
@@ -455,7 +480,8 @@ def main(argv=None):
                                "(every env's steps back to back, its book kept in LDS)" if args.slices == 0 else
                                f"{args.slices} env slices on their own streams, {T} steps per rollout_sampled call")
                               if args.mode == "rollout" else "split_keys + sample_actions + env.step per step"),
-                   "mode": args.mode, "seeds": "Speed_test: split(PRNGKey(0), NUM_ENVS + 1)"},
+                   "mode": args.mode, "seeds": "Speed_test: split(PRNGKey(0), NUM_ENVS + 1)",
+                   "timed_window": timed_window(args.steps, max_steps, ctr0)},
         "roofline": roofline,
         "issue_roofline": issue,
         "cpu_baseline": cpu,

@@ -328,6 +328,13 @@ int hftlob_env_rollout_sampled(const hftlob_env_cfg* cfg /*[host]*/, int n_env, 
  * slices on the device of `stream` (host-only; idempotent). */
 int hftlob_rollout_prepare(int n_slices, void* stream);
 
+/* Dynamic LDS bytes of one env's workgroup in hftlob_env_step / hftlob_env_rollout_sampled
+ * for this config (agent rows, action extras, book sides, trade log, pad / filter / scratch rows
+ * and the rollout's step-key batches), or a negative HFTLOB_E* code for an invalid cfg
+ * (host-only, no device call).  Hosts size launch shapes from it (how many envs a CU holds at
+ * once); it replaces nothing in the reference, whose XLA compiler sizes its own buffers. */
+int hftlob_env_lds_bytes(const hftlob_env_cfg* cfg /*[host]*/);
+
 /* Speed_test action sampling (Speed_test.py:166-177, gymnax Discrete.sample):
  * for env e with step key k_e,
  * sub = split(k_e, n_types); per type t, agent i:

@@ -3032,15 +3032,20 @@ typedef const __attribute__((address_space(4))) hftlob_env_cfg kcfg_t;
 // is zero-initialised device memory of the code object (no allocation).  Scheduling only: no
 // result depends on it.
 #define WAVE_SLOTS (8 * 16 * 16 * 64)  // XCC (8) x SE (8) x SH (2) x CU (16), x 64 wave slots per CU
-__device__ unsigned long long g_wave_eta[WAVE_SLOTS];
+static __device__ unsigned long long g_wave_eta[WAVE_SLOTS];  // (static: one per translation unit of the split build)
+// the CU's row of the table (64 wave slots) and this wave's slot in it (SIMD * 16 + wave id)
+DEV unsigned long long* wave_row(u32 hwid, u32 xcc, u32& slot) {
+    const u32 cu = ((xcc & 7u) * 16u + ((hwid >> 13) & 7u) * 2u + ((hwid >> 12) & 1u)) * 16u + ((hwid >> 8) & 15u);
+    slot = ((hwid >> 4) & 3u) * 16u + (hwid & 15u);
+    return g_wave_eta + (size_t)cu * 64u;
+}
 DEV void balance_prio(u32 hwid, u32 xcc, unsigned long long r0, int done, int left) {
     const int l = lane_id();
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const float el = (float)(now - r0);
     const unsigned long long eta = now + (unsigned long long)(el * ((float)left / (float)done));
-    const u32 cu = ((xcc & 7u) * 16u + ((hwid >> 13) & 7u) * 2u + ((hwid >> 12) & 1u)) * 16u + ((hwid >> 8) & 15u);
-    const u32 slot = ((hwid >> 4) & 3u) * 16u + (hwid & 15u);
-    unsigned long long* row = g_wave_eta + (size_t)cu * 64u;
+    u32 slot;
+    unsigned long long* row = wave_row(hwid, xcc, slot);
     if (l == 0) __hip_atomic_store(row + slot, eta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long v = __hip_atomic_load(row + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     v = (u32)l == slot ? eta : v;
@@ -3098,7 +3103,9 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         const i32* is = init_states;
         asm volatile("" : "+s"(cp), "+s"(st), "+s"(md), "+s"(is));
         const hftlob_env_cfg& cc = *(const hftlob_env_cfg*)cp;
+        STAMP(kb0);
         if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
+        STAMP(kb1);
         const bool reset = env_step_dev<S, NFIX, RC>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
@@ -3108,8 +3115,18 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
             out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds, NFIX > 0 && resident,
             NFIX > 0 && t + 1 < n_steps, fl, kbat ? kbuf + tb * kbw : nullptr);
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
+        STAMP(bp0);
 #ifndef HFTLOB_NO_BALANCE
         if (t + 1 < n_steps) balance_prio(bal_hwid, bal_xcc, bal_r0, t + 1, n_steps - t - 1);
+#endif
+#ifdef HFTLOB_STAMPS
+        // rollout-only phases beside env_step_dev's stamps: the step-key batch (every KB_STEPS-th
+        // step) and the issue-priority update, words 16 / 17 of the step's info row
+        if (out.info && per_step && lane_id() == 0) {
+            i32* irow = out.info + ((size_t)t * n_env + e) * cc.info_words;
+            irow[16] = (i32)(kb1 - kb0);
+            irow[17] = (i32)(__builtin_amdgcn_s_memtime() - bp0);
+        }
 #endif
 #ifdef HFTLOB_WAVETIME
         if (out.info && per_step) {
@@ -3124,10 +3141,19 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         }
 #endif
     }
+#ifndef HFTLOB_NO_BALANCE
+    {  // the wave is done: its slot's entry becomes a past time, so no neighbour counts it as live
+        u32 slot;
+        unsigned long long* row = wave_row(bal_hwid, bal_xcc, slot);
+        if (lane_id() == 0) __hip_atomic_store(row + slot, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
 
 // ==================================================== K3/K4: PRNG kernels
+#if !defined(HFTLOB_INST)  // (non-template kernels: the main translation unit only)
 __global__ void k_sample_actions(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys, i32* __restrict__ actions) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n_env) return;
@@ -3154,6 +3180,48 @@ __global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__
     out[2 * (size_t)t] = o.a;
     out[2 * (size_t)t + 1] = o.b;
 }
+
+#endif  // !HFTLOB_INST
+
+// ============================================ instantiations (parallel build)
+// The Makefile compiles this file HFTLOB_NPARTS + 1 times: part k (HFTLOB_INST = k) explicitly
+// instantiates its share of the env-step / rollout kernels, the main translation unit (no
+// HFTLOB_INST) declares them extern and holds the small kernels and the C ABI.
+#define HFTLOB_STEP_ARGS hftlob_env_cfg, int, int, int, const u32*, const u32*, u32*, i32*, const i32*, const i32*, i32*, \
+                         hftlob_step_out
+#define HFTLOB_ROLL_ARGS hftlob_env_cfg, int, int, int, int, int, const u32*, u32*, i32*, const i32*, const i32*, i32*, \
+                         hftlob_step_out
+#define HFTLOB_STEP(P, SS, NF, RC) P template __global__ void k_env_step<SS, NF, RC>(HFTLOB_STEP_ARGS);
+#define HFTLOB_ROLL(P, SS, NF, RC) P template __global__ void k_env_rollout<SS, NF, RC>(HFTLOB_ROLL_ARGS);
+#define HFTLOB_PART1(P) HFTLOB_ROLL(P, 2, 100, false)
+#define HFTLOB_PART2(P) HFTLOB_STEP(P, 2, 100, false)
+#define HFTLOB_PART3(P) HFTLOB_ROLL(P, 1, 0, false) HFTLOB_STEP(P, 1, 0, false)
+#define HFTLOB_PART4(P) HFTLOB_ROLL(P, 2, 0, false) HFTLOB_STEP(P, 2, 0, false)
+#define HFTLOB_PART5(P) HFTLOB_ROLL(P, 4, 0, false) HFTLOB_STEP(P, 4, 0, false)
+#define HFTLOB_PART6(P) HFTLOB_ROLL(P, 1, 0, true) HFTLOB_STEP(P, 1, 0, true) HFTLOB_ROLL(P, 2, 0, true)
+#define HFTLOB_PART7(P) HFTLOB_STEP(P, 2, 0, true) HFTLOB_ROLL(P, 4, 0, true) HFTLOB_STEP(P, 4, 0, true)
+#define HFTLOB_NONE
+#if defined(HFTLOB_INST)
+#if HFTLOB_INST == 1
+HFTLOB_PART1(HFTLOB_NONE)
+#elif HFTLOB_INST == 2
+HFTLOB_PART2(HFTLOB_NONE)
+#elif HFTLOB_INST == 3
+HFTLOB_PART3(HFTLOB_NONE)
+#elif HFTLOB_INST == 4
+HFTLOB_PART4(HFTLOB_NONE)
+#elif HFTLOB_INST == 5
+HFTLOB_PART5(HFTLOB_NONE)
+#elif HFTLOB_INST == 6
+HFTLOB_PART6(HFTLOB_NONE)
+#elif HFTLOB_INST == 7
+HFTLOB_PART7(HFTLOB_NONE)
+#endif
+#else  // the main translation unit
+#if !defined(HFTLOB_SINGLE_TU)
+HFTLOB_PART1(extern) HFTLOB_PART2(extern) HFTLOB_PART3(extern) HFTLOB_PART4(extern)
+HFTLOB_PART5(extern) HFTLOB_PART6(extern) HFTLOB_PART7(extern)
+#endif
 
 // ================================================================ C ABI
 static thread_local char g_err[256] = "";
@@ -3432,6 +3500,11 @@ static int rollout_ctx(int dev, int G, RolloutCtx** out) {
     return HFTLOB_OK;
 }
 
+int hftlob_env_lds_bytes(const hftlob_env_cfg* cfg) {
+    const int rc = check_env(cfg);
+    return rc ? rc : (int)env_shm(cfg);
+}
+
 int hftlob_rollout_prepare(int n_slices, void* stream) {
     if (n_slices < 0 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 0..4");
     if (n_slices <= 1) return HFTLOB_OK;  // no library stream needed
@@ -3525,3 +3598,4 @@ int hftlob_split_keys(int n_env, int n, int partitionable, const uint32_t* keys,
 }
 
 }  // extern "C"
+#endif  // the main translation unit

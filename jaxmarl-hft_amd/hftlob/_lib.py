@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.
 ABI_VERSION = 7
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
            "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_env_rollout_sampled", "hftlob_rollout_prepare",
+           "hftlob_env_lds_bytes",
            "hftlob_sample_actions", "hftlob_split_keys")
 
 _lib = None
@@ -49,6 +50,8 @@ def lib() -> C.CDLL:
     L.hftlob_env_rollout_sampled.restype = i32
     L.hftlob_rollout_prepare.argtypes = [i32, vp]
     L.hftlob_rollout_prepare.restype = i32
+    L.hftlob_env_lds_bytes.argtypes = [C.POINTER(EnvCfg)]
+    L.hftlob_env_lds_bytes.restype = i32
     L.hftlob_sample_actions.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp]
     L.hftlob_sample_actions.restype = i32
     L.hftlob_split_keys.argtypes = [i32, i32, i32, vp, vp, vp]

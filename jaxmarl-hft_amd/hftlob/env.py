@@ -377,9 +377,26 @@ class MARLEnv:
 
     def _abi(self, fn: str, *args):
         """Call libhftlob `fn` with this env's device current and torch's current stream OF THAT
-        DEVICE appended (the kernels, and the rollout's slice streams, follow the stream)."""
-        with torch.cuda.device(self.device):
-            _lib.check(getattr(_lib.lib(), fn)(*args, _lib.stream_ptr(device=self.device)))
+        DEVICE appended (the kernels, and the rollout's slice streams, follow the stream).  The
+        device context is entered only when another device is current (it costs host time
+        before every launch, and the bench's timed region starts before the launch)."""
+        f = getattr(_lib.lib(), fn)
+        dev = self._dev_index
+        if torch.cuda.current_device() == dev:
+            rc = f(*args, torch.cuda.current_stream(dev).cuda_stream)
+        else:
+            with torch.cuda.device(dev):
+                rc = f(*args, torch.cuda.current_stream(dev).cuda_stream)
+        if rc:
+            _lib.check(rc)
+
+    @property
+    def _dev_index(self) -> int:
+        i = self.__dict__.get("_dev_idx")
+        if i is None:
+            i = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            self.__dict__["_dev_idx"] = i
+        return i
 
     # ------------------------------------------------------------------ API
     def reset(self, key: torch.Tensor, params: Optional[MultiAgentParams] = None):
@@ -434,21 +451,26 @@ class MARLEnv:
         return self._results(o, state, E)
 
     LDS_PER_CU = 160 * 1024      # MI355X (gfx950) LDS per CU
-    ROLLOUT_WAVES_PER_CU = 16    # k_env_rollout: launch_bounds(64, 4), ~105 VGPRs -> 4 waves per SIMD
+    ROLLOUT_WAVES_PER_CU = 16    # k_env_rollout: launch_bounds(64, 4), 128 VGPRs -> 4 waves per SIMD
+    TUNED_ARCH = "gfx950"        # the device the launch-shape rule below was measured on
 
     def lds_bytes_per_env(self) -> int:
-        """Dynamic LDS of one env's workgroup (env_shm in hftlob.hip): agent rows, action extras,
-        the two book sides, the trade log, the pad / filter / scratch rows and the rollout's key
-        batches."""
-        c = self.cfg_c
-        kb = (4 * (6 + c.n_agents + c.n_action_msgs)   # the rollout's key batches (step_keys_batch)
-              if c.prng_partitionable and c.n_agents <= 3 and c.n_action_msgs <= 8 and c.n_types <= 6
-              and 6 + c.n_agents + c.n_action_msgs <= 16 else 0)
-        return 4 * ((c.n_cancel_msgs + c.n_action_msgs) * 8 + ((c.n_agents * 6 + 3) & ~3) +
-                    12 * c.lob.n_orders + 8 * c.lob.n_trades + 64 * 4 + kb)
+        """Dynamic LDS of one env's workgroup, from the library (hftlob_env_lds_bytes: env_shm in
+        hftlob.hip, the figure its launches use): agent rows, action extras, the two book sides,
+        the trade log, the pad / filter / scratch rows and the rollout's key batches."""
+        n = int(_lib.lib().hftlob_env_lds_bytes(C.byref(self.cfg_c)))
+        if n <= 0:
+            _lib.check(n)
+        return n
+
+    def _tuned_device(self) -> bool:
+        if not torch.cuda.is_available():
+            return True
+        return torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0] == self.TUNED_ARCH
 
     def resident_envs(self) -> int:
-        """Envs of this config the GPU holds at once (workgroups per CU by LDS and by waves)."""
+        """Envs of this config the GPU holds at once (workgroups per CU by LDS and by waves; the
+        MI355X figures above)."""
         per_cu = min(self.ROLLOUT_WAVES_PER_CU, self.LDS_PER_CU // self.lds_bytes_per_env())
         n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count \
             if torch.cuda.is_available() else 256
@@ -464,7 +486,10 @@ class MARLEnv:
         against 7.7 / 28.6 / 47.8 / 59.7 / 61.6 M for 2 slices); 2 env slices on their own streams
         when the last wave would be partly empty, as its envs would run whole rollouts after the
         others finish (Speed_test's [5,5] / [10,10] agents at 4000 envs, whose agent rows leave
-        room for 14 / 11 envs per CU: 25.1 / 15.7 M against 19.7 / 12.3 M)."""
+        room for 14 / 11 envs per CU: 25.1 / 15.7 M against 19.7 / 12.3 M).  On a device other
+        than the one this was measured on, 2 slices (they never wait for whole rollouts)."""
+        if not self._tuned_device():  # LDS / wave limits of another device are not known here
+            return 2
         cap = self.resident_envs()
         if n_env <= cap:
             return 0
@@ -513,7 +538,8 @@ class MARLEnv:
             raise ValueError(f"actions_out must be int32 {list(shape)}")
         self._abi("hftlob_env_rollout_sampled", C.byref(self.cfg_c), E, int(key_e0),
                   int(E if key_n is None else key_n), n_steps, _lib.ptr(key_in), _lib.ptr(key_out),
-                  _lib.ptr(self._key_scratch()), _lib.ptr(actions_out), _lib.ptr(params.loaded_params.message_data),
+                  _lib.ptr(self._key_scratch()) if n_slices else None,  # (the persistent launch needs none)
+                  _lib.ptr(actions_out), _lib.ptr(params.loaded_params.message_data),
                   _lib.ptr(params.loaded_params.init_states_array), _lib.ptr(state.buf), C.byref(o["struct"]),
                   int(per_step), int(n_slices))
         if not per_step:

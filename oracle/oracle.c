@@ -1487,9 +1487,11 @@ static i32 volume_at(const i32* s, int nO, i32 p) {
     for (int i = 0; i < nO; ++i) if (s[i * 6] == p) v = wadd(v, s[i * 6 + 1]);
     return v;
 }
-void oracle_l2_state(const hftlob_lob_cfg* c, const i32* asks, const i32* bids, int n_levels, i32* out) {
+int oracle_l2_state(const hftlob_lob_cfg* c, const i32* asks, const i32* bids, int n_levels, i32* out) {
     int nO = c->n_orders;
     i32 tmp[HFTLOB_MAX_SLOTS], lv[HFTLOB_MAX_SLOTS];
+    /* the stack tables hold HFTLOB_MAX_SLOTS rows / levels (the env path refuses larger books) */
+    if (nO < 1 || nO > HFTLOB_MAX_SLOTS || n_levels < 0 || n_levels > HFTLOB_MAX_SLOTS) return HFTLOB_ESHAPE;
     for (int i = 0; i < nO; ++i) tmp[i] = wmul(-1, bids[i * 6]);
     unique_sorted(tmp, nO, n_levels, 1, lv);
     for (int k = 0; k < n_levels; ++k) {
@@ -1507,6 +1509,7 @@ void oracle_l2_state(const hftlob_lob_cfg* c, const i32* asks, const i32* bids, 
         out[k * 4] = p;
         out[k * 4 + 1] = q < 0 ? 0 : q;
     }
+    return HFTLOB_OK;
 }
 
 /* ---- MARLEnv.step — marl_env.py:775-804 + step_env :211-709 */

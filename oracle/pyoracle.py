@@ -30,6 +30,7 @@ def _bind(L):
     L.oracle_env_step_ex.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_env_step_dbg.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.oracle_l2_state.argtypes = [vp, vp, vp, C.c_int, vp]
+    L.oracle_l2_state.restype = C.c_int
     L.oracle_sample_actions.argtypes = [vp, C.c_int, vp, vp]
     L.oracle_mm_action_msgs.argtypes = [vp, C.c_int, C.c_int, vp, vp, vp, vp]
     L.oracle_split_keys.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp]
@@ -146,9 +147,12 @@ def env_step(env_cfg, keys, actions, msg_data, init_states, state, with_info=Tru
 
 def l2_state(lob_cfg, asks, bids, n_levels=10):
     """get_L2_state (JaxOrderBookArrays.py:1231-1264) of one book: int32 [n_levels * 4]."""
-    out = np.zeros(n_levels * 4, np.int32)
-    lib().oracle_l2_state(C.byref(lob_cfg), _p(np.ascontiguousarray(asks, np.int32)),
-                          _p(np.ascontiguousarray(bids, np.int32)), int(n_levels), _p(out))
+    out = np.zeros(max(n_levels, 0) * 4, np.int32)
+    asks = np.ascontiguousarray(asks, np.int32)
+    bids = np.ascontiguousarray(bids, np.int32)
+    if asks.size < lob_cfg.n_orders * 6 or bids.size < lob_cfg.n_orders * 6:
+        raise ValueError("l2_state: asks / bids hold fewer than n_orders rows")
+    _chk(lib().oracle_l2_state(C.byref(lob_cfg), _p(asks), _p(bids), int(n_levels), _p(out)))
     return out
 
 

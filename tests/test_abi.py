@@ -140,3 +140,29 @@ def test_device_tensors_required():
     import torch
     with pytest.raises(RuntimeError, match="device"):
         _lib.ptr(torch.zeros(4, dtype=torch.int32))
+
+
+@pytest.mark.parametrize("name,agents,part,kb", [("2_player_fq_fqc", None, True, True),
+                                                 ("2_player_fq_fqc", None, False, False),
+                                                 ("3_player_fq_fqc_dir", None, True, False),
+                                                 ("default", [1, 1], True, True),
+                                                 ("default", [5, 5], True, False),
+                                                 ("default", [10, 10], True, False)])
+def test_env_lds_bytes(L, name, agents, part, kb):
+    """hftlob_env_lds_bytes (the LDS the step / rollout launches reserve per env, which
+    MARLEnv.resident_envs sizes launch shapes from) on both sides of the rollout's key-batch rule
+    (kb_ok: partitionable keys, <= 3 agents, <= 8 action rows, 6 + agents + rows <= 16):
+    [rows (C+A)*8][action extras][asks 6 nO][bids 6 nO][trades 8 nT][pad 64*4][key batches 4 x row]."""
+    import dataclasses
+    cfg = builtin_config(name)
+    if agents:
+        cfg = dataclasses.replace(cfg, number_of_agents_per_type=agents)
+    c, _ = pack_env_cfg(cfg, 4, 1000, part)
+    ok = (part and c.n_agents <= 3 and c.n_action_msgs <= 8 and c.n_types <= 6
+          and 6 + c.n_agents + c.n_action_msgs <= 16)
+    assert ok == kb
+    want = 4 * ((c.n_cancel_msgs + c.n_action_msgs) * 8 + ((c.n_agents * 6 + 3) & ~3) + 12 * c.lob.n_orders
+                + 8 * c.lob.n_trades + 64 * 4 + (4 * (6 + c.n_agents + c.n_action_msgs) if kb else 0))
+    assert L.hftlob_env_lds_bytes(C.byref(c)) == want
+    c.ep_type = 2
+    assert L.hftlob_env_lds_bytes(C.byref(c)) == -1   # an invalid cfg: its error code

@@ -41,3 +41,13 @@ def test_failing_rank_fails_the_launch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--envs", "x"],
                        capture_output=True, text=True, env=env, timeout=120, cwd=ROOT)
     assert r.returncode != 0
+
+
+def test_timed_window():
+    """config.timed_window: the driver's 20-step window from the reset state never reaches the
+    64-step episode's end (marl_env.py:711-718 fires at step counter 62); 128 steps cross two."""
+    import bench
+    assert "no episode end" in bench.timed_window(20, 64)
+    assert "at timed step(s) [62, 125]" in bench.timed_window(128, 64)
+    assert "at timed step(s) [62]" in bench.timed_window(63, 64)
+    assert "no episode end" in bench.timed_window(62, 64)

@@ -89,6 +89,23 @@ def test_l2_state_oracle_vs_numpy():
         assert np.array_equal(O.l2_state(lc, a, b), l2_numpy(a, b))
 
 
+def test_l2_state_refuses_oversized_tables():
+    """oracle_l2_state's stack tables hold HFTLOB_MAX_SLOTS (256) rows / levels: a larger
+    n_levels or n_orders is refused with HFTLOB_ESHAPE instead of overflowing them."""
+    lc = pack_lob_cfg(JAXLOB_Configuration())
+    a = b = np.full((100, 6), -1, I32)
+    with pytest.raises(RuntimeError, match="-3"):
+        O.l2_state(lc, a, b, n_levels=257)
+    big = np.full((300, 6), -1, I32)
+    lc.n_orders = 300
+    with pytest.raises(RuntimeError, match="-3"):
+        O.l2_state(lc, big, big)
+    lc.n_orders = 100
+    with pytest.raises(ValueError):
+        O.l2_state(lc, a[:50], b)
+    assert O.l2_state(lc, a, b, n_levels=256).shape == (1024,)
+
+
 def _debug_cfg(name="2_player_fq_fqc"):
     cfg = builtin_config(name)
     return dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, debug_mode=True))

@@ -79,6 +79,42 @@ def test_rollout_shards_equal_whole_batch():
         assert (s.buf == whole.buf[r * E:(r + 1) * E]).all(), f"rank {r}: state"
 
 
+@pytest.mark.parametrize("name,E,part", [("2_player_fq_fqc", 4096, True), ("2_player_fq_fqc", 4096, False),
+                                         ("3_player_fq_fqc_dir", 1024, True), ("3_player_fq_fqc_dir", 1024, False)])
+def test_rank_shard_at_real_size(name, E, part):
+    """The last rank's shard of the 8-GPU configs at their real sizes and key offsets, on one GPU
+    (BASELINE.json configs C4 / C5; ippo_rnn_JAXMARL_pmap.py:292-332, Speed_test.py:142-147):
+    C4 = 2_player_fq_fqc, NUM_ENVS = 32768 over 8 ranks, rank 7 steps envs [7*4096, 8*4096);
+    C5 = 3_player_fq_fqc_dir (MM + EXE + directional), NUM_ENVS = 8192, rank 7 steps [7*1024, 8*1024).
+    Reset keys split(PRNGKey(0), N*E + 1)[1 + 7E : 1 + 8E], step keys split(master, N*E + 1)[1 + 7E + e]
+    (key_e0 = 7E, key_n = N*E), 66 steps (every env crosses its episode end) with the launch shape the
+    bench picks for E envs per GPU, partitionable and legacy threefry (with the legacy split, key_n
+    changes every key).  End state and carried master key against the CPU oracle's rollout."""
+    N, r, T = 8, 7, 66
+    cfg = builtin_config(name)
+    w = cfg.world_config
+    day = generate_day(n_msgs=400_000, mid=2_000_000, snap_every=w.n_data_msg_per_step * w.start_resolution)
+    env = MARLEnv(None, cfg, data=day, prng_partitionable=part, return_info=False, persistent_outputs=True)
+    params = env.default_params
+    init = env._init_states.cpu().numpy()
+    assert (init == O.init_states(env.cfg_c.lob, env.windows, day.msgs, w, env.layout.init_rec_words)).all()
+    all_keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device="cuda"), N * E + 1, part)[0]
+    o_keys = O.split_keys(np.zeros((1, 2), np.uint32), N * E + 1, part)[0]
+    assert (all_keys.cpu().numpy().view(np.uint32) == o_keys).all(), "Speed_test key split over N*E envs"
+    rows = slice(1 + r * E, 1 + (r + 1) * E)
+    _, state = env.reset(all_keys[rows].contiguous(), params)
+    o_state, _ = O.env_reset(env.cfg_c, o_keys[rows], init)
+    _compare_state(env, o_state, state.buf.cpu().numpy(), "reset")
+    G = env.default_slices(E)
+    kin, kout = all_keys[0].clone(), torch.empty(2, dtype=torch.int32, device="cuda")
+    env.rollout_sampled(kin, kout, state, params, T, n_slices=G, key_e0=r * E, key_n=N * E)
+    torch.cuda.synchronize()
+    o_end, o_master = O.rollout_sampled(env.cfg_c, o_keys[0], day.msgs, init, o_state, T, key_e0=r * E, key_n=N * E)
+    _compare_state(env, o_end, state.buf.cpu().numpy(), f"rank {r} shard after {T} steps (slices {G})")
+    assert (kout.cpu().numpy().view(np.uint32) == o_master).all(), "carried master key"
+    assert (state.world_state.step_counter.cpu().numpy() < T).all()
+
+
 def test_default_launch_shape():
     """MARLEnv.default_slices: the persistent launch while its waves of workgroups are full (the
     metric: 4096 envs at 16 per CU, and whole multiples of it), 2 env slices when the last wave

@@ -45,6 +45,22 @@ for _ in range(30):
     wall.append(t2 - t0)
     host.append(t1 - t0)
     ev.append(e0.elapsed_time(e1) * 1e-3)
+# the same launch as one bare ctypes call with its arguments prepared beforehand: the floor of
+# the host path (what the Python wrapper adds is the difference to "host call")
+import ctypes as C  # noqa: E402
+from hftlob import _lib  # noqa: E402
+o = env._outputs(E)
+L = _lib.lib()
+args = (C.byref(env.cfg_c), E, 0, E, T, k0.data_ptr(), k1.data_ptr(), None, None,
+        params.loaded_params.message_data.data_ptr(), params.loaded_params.init_states_array.data_ptr(),
+        state.buf.data_ptr(), C.byref(o["struct"]), 0, 0, torch.cuda.current_stream().cuda_stream)
+bare = []
+for _ in range(30):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    L.hftlob_env_rollout_sampled(*args)
+    bare.append(time.perf_counter() - t0)
+torch.cuda.synchronize()
 # a synchronised empty round trip (event record + synchronize): the completion latency floor
 rt = []
 for _ in range(30):
@@ -55,4 +71,5 @@ for _ in range(30):
     rt.append(time.perf_counter() - t0)
 med = lambda x: float(np.median(x)) * 1e6  # noqa: E731
 print(f"steps {T}: wall {med(wall):.1f} us, events {med(ev):.1f} us, host call {med(host):.1f} us, "
-      f"empty sync round trip {med(rt):.1f} us, wall - events {med(wall) - med(ev):.1f} us")
+      f"empty sync round trip {med(rt):.1f} us, wall - events {med(wall) - med(ev):.1f} us, "
+      f"bare ctypes launch call {med(bare):.1f} us")
