@@ -200,7 +200,9 @@ typedef struct hftlob_env_cfg {
     int32_t off_best_bids, off_best_asks, off_world, off_agents;
     int32_t info_words;            /* words per env in the optional info buffer */
     int32_t action_words;          /* sum_t n_agents_t * action_width_t: int32 words per env of actions */
-    int32_t _pad[1];
+    /* set by the library before each env launch (a caller's value is ignored): the multiplier of
+       the exact floor division by tick_size, ceil(2^(31+l) / tick_size), l = ceil(log2 tick_size) */
+    uint32_t tick_magic;
     hftlob_agent_type_cfg types[HFTLOB_MAX_TYPES];
 } hftlob_env_cfg;
 

@@ -56,6 +56,18 @@ DEV i32 ifloordiv(i32 a, i32 b) {
     if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
     return q;
 }
+// jnp.floor_divide(a, tick_size), exactly, by a multiply: with l = ceil(log2 d) and
+// m = ceil(2^(31+l) / d) < 2^32 (hftlob_env_cfg.tick_magic, set by the launch code),
+// floor(n / d) = (n * m) >> (31 + l) for every 0 <= n < 2^31 (Granlund & Montgomery 1994, thm 4.2,
+// N = 31); a negative a divides ~a = -a - 1 and the quotient's complement is the floor
+// (tools/magic_check.c checks every int32 numerator for d = 1, 3, 100)
+DEV i32 tick_floordiv(const hftlob_env_cfg& c, i32 a) {
+    const u32 d = (u32)c.tick_size;
+    const int sh = 31 + (d > 1u ? 32 - __builtin_clz(d - 1u) : 0);
+    const u32 n = a < 0 ? ~(u32)a : (u32)a;
+    const u32 q = (u32)(((unsigned long long)n * c.tick_magic) >> sh);
+    return a < 0 ? (i32)~q : (i32)q;
+}
 // fmodf, exactly, without the library's bit-by-bit reduction loop when |x / y| < 2^23 (prices
 // over a tick): with the correctly rounded quotient q' of |x| / |y| < 2^23, trunc(q') is the true
 // quotient Q or Q + 1 (Q and Q + 1 are floats and rounding is monotonic), so |x| - trunc(q')|y|
@@ -1728,8 +1740,8 @@ DEV bool masked_best(const hftlob_env_cfg& c, Book<S>& B, i32 tid, i32 last_ba, 
     bb = wave_max(mx);
     ba = ba == c.lob.maxint ? -1 : ba;
     const bool empty = (ba == -1) || (bb == -1);
-    ba = wmul(ifloordiv(ba, tick), tick);
-    bb = wmul(ifloordiv(bb, tick), tick);
+    ba = wmul(tick_floordiv(c, ba), tick);
+    bb = wmul(tick_floordiv(c, bb), tick);
     if (empty) { bb = last_bb; ba = last_ba; }
     return empty;
 }
@@ -1834,14 +1846,14 @@ DEV void mm_other_actions(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& 
             af = fminf(fmaxf(af, 0.0f), (float)c.lob.maxint);
             bp = f2i_sat(ffloordiv(bf, (float)tick) * (float)tick);
             ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
-            const i32 q = ifloordiv(mid, tick), rm = wsub(mid, wmul(q, tick));
+            const i32 q = tick_floordiv(c, mid), rm = wsub(mid, wmul(q, tick));
             bp = imin_(bp, wmul(wsub(q, rm == 0 ? 1 : 0), tick));  // round_down: strictly below mid
             ap = imax_(ap, wmul(wadd(q, 1), tick));                // round_up: strictly above mid
             bq = fq; aq = fq;
             bdist = wsub(bb, bp); adist = wsub(ap, ba); bpost = bp; apost = ap;
         }
     } else {
-        const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
+        const i32 ba = wmul(tick_floordiv(c, last_ba), tick), bb = wmul(tick_floordiv(c, last_bb), tick);
         if (kind == HFTLOB_MM_ACT_SPREAD_SKEW) {  // :1667-1808
             const float mid = i2f(wadd(ba, bb)) / 2.0f;
             const i32 cur = wsub(ba, bb);
@@ -1883,7 +1895,7 @@ DEV void mm_other_actions(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& 
 DEV void mm_directional(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, i32 tid, i32 action, i32 wt0, i32 wt1,
                         i32 last_ba, i32 last_bb, i32* lds_rows, int row, ActX& x) {
     const i32 tick = c.tick_size;
-    const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
+    const i32 ba = wmul(tick_floordiv(c, last_ba), tick), bb = wmul(tick_floordiv(c, last_bb), tick);
     const int ai = action < 0 ? imax_(action + 3, 0) : (action > 2 ? 2 : action);
     const i32 bq = (ai == 1) * tc.fixed_quant_value, aq = (ai == 2) * tc.fixed_quant_value;
     const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
@@ -1898,7 +1910,7 @@ DEV void mm_directional(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
 DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const i32* st, i32 tid, i32 action, i32 wt0,
                  i32 wt1, i32 last_ba, i32 last_bb, i32 step, i32 max_steps, i32* lds_rows, int row) {
     const i32 tick = c.tick_size;
-    const i32 ba = wmul(ifloordiv(last_ba, tick), tick), bb = wmul(ifloordiv(last_bb, tick), tick);
+    const i32 ba = wmul(tick_floordiv(c, last_ba), tick), bb = wmul(tick_floordiv(c, last_bb), tick);
     const i32 sell = st[3];
     i32 pl[4];
     if (sell) {
@@ -1908,7 +1920,7 @@ DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
         pl[3] = wadd(ba, wmul(tick, tc.n_ticks_in_book));
     } else {
         pl[0] = ba;
-        pl[1] = wmul(ifloordiv(ifloordiv(wadd(bb, ba), 2), tick), tick);
+        pl[1] = wmul(tick_floordiv(c, ifloordiv(wadd(bb, ba), 2)), tick);
         pl[2] = bb;
         pl[3] = wsub(bb, wmul(tick, tc.n_ticks_in_book));
     }
@@ -1982,13 +1994,13 @@ DEV void exe_fixed_prices(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& 
     const i32 ba = f2i_sat(ffloordiv(sa / n, ft) * ft), bb = f2i_sat(ffloordiv(sb / n, ft) * ft);
     i32 lv[4];  // FT, M, NT, PP
     if (sell) {
-        lv[0] = wmul(ifloordiv(bb, tick), tick);
+        lv[0] = wmul(tick_floordiv(c, bb), tick);
         lv[1] = f2i_sat(ceilf(ffloordiv(i2f(wadd(bb, ba)) / 2.0f, ft)) * ft);
         lv[2] = ba;
         lv[3] = wadd(ba, wmul(tick, tc.n_ticks_in_book));
     } else {
-        lv[0] = wmul(ifloordiv(ba, tick), tick);
-        lv[1] = wmul(ifloordiv(ifloordiv(wadd(bb, ba), 2), tick), tick);
+        lv[0] = wmul(tick_floordiv(c, ba), tick);
+        lv[1] = wmul(tick_floordiv(c, ifloordiv(wadd(bb, ba), 2)), tick);
         lv[2] = bb;
         lv[3] = wsub(bb, wmul(tick, tc.n_ticks_in_book));
     }
@@ -2245,8 +2257,8 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
         i32 refp;
         const float penf = tc.doom_penalty_is_float ? tc.doom_penalty_f32 : i2f(pen);
         if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH && !tc.doom_penalty_is_float)
-            refp = sell ? wmul(ifloordiv(wsub(X.last_bb, pen), tick), tick)
-                        : wmul(ifloordiv(wadd(X.last_ba, pen), tick), tick);
+            refp = sell ? wmul(tick_floordiv(c, wsub(X.last_bb, pen)), tick)
+                        : wmul(tick_floordiv(c, wadd(X.last_ba, pen)), tick);
         else if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)  // int32 price - Python float: f32
             refp = sell ? f2i(ffloordiv(i2f(X.last_bb) - penf, (float)tick) * (float)tick)
                         : f2i(ffloordiv(i2f(X.last_ba) + penf, (float)tick) * (float)tick);
@@ -2267,7 +2279,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
         const bool mine = V.valid[r] && (tid == V.PT[r] || tid == V.AT[r]);
         aq = wadd(aq, mine ? iabs_(V.Q[r]) : 0);
         oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
-        qp = wadd(qp, mine ? wmul(ifloordiv(V.P[r], tick), iabs_(V.Q[r])) : 0);
+        qp = wadd(qp, mine ? wmul(tick_floordiv(c, V.P[r]), iabs_(V.Q[r])) : 0);
         dur[r] = mine ? i2f(iabs_(V.Q[r])) / i2f(task) * i2f(wsub(V.S4[r], X.init0))
                       : i2f(0) / i2f(task) * i2f(wsub(0, X.init0));
     }
@@ -2280,7 +2292,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
         for (int r = 0; r < S; ++r) {
             const bool other = V.valid[r] && !(tid == V.PT[r] || tid == V.AT[r]);
             const i32 P = other ? V.P[r] : 0, Q = other ? V.Q[r] : 0;
-            vw[r] = i2f(ifloordiv(P, tick)) * (i2f(iabs_(Q)) / i2f(oq));
+            vw[r] = i2f(tick_floordiv(c, P)) * (i2f(iabs_(Q)) / i2f(oq));
         }
         pv = rows_fsum(vw, nT);
     }
@@ -3039,13 +3051,11 @@ DEV unsigned long long* wave_row(u32 hwid, u32 xcc, u32& slot) {
     slot = ((hwid >> 4) & 3u) * 16u + (hwid & 15u);
     return g_wave_eta + (size_t)cu * 64u;
 }
-DEV void balance_prio(u32 hwid, u32 xcc, unsigned long long r0, int done, int left) {
+DEV void balance_prio(unsigned long long* row, u32 slot, unsigned long long r0, int done, int left) {
     const int l = lane_id();
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const float el = (float)(now - r0);
     const unsigned long long eta = now + (unsigned long long)(el * ((float)left / (float)done));
-    u32 slot;
-    unsigned long long* row = wave_row(hwid, xcc, slot);
     if (l == 0) __hip_atomic_store(row + slot, eta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long v = __hip_atomic_load(row + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     v = (u32)l == slot ? eta : v;
@@ -3081,6 +3091,8 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
 #ifndef HFTLOB_NO_BALANCE
     const unsigned long long bal_r0 = __builtin_amdgcn_s_memrealtime();
     const u32 bal_hwid = __builtin_amdgcn_s_getreg(0xF804), bal_xcc = __builtin_amdgcn_s_getreg(0x7814);
+    u32 bal_slot;
+    unsigned long long* bal_row = wave_row(bal_hwid, bal_xcc, bal_slot);
 #endif
 #ifdef HFTLOB_WAVETIME
     // diagnostic build only (tools/diag_wavetime.py): the wave's start time and hardware slot,
@@ -3117,7 +3129,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
         STAMP(bp0);
 #ifndef HFTLOB_NO_BALANCE
-        if (t + 1 < n_steps) balance_prio(bal_hwid, bal_xcc, bal_r0, t + 1, n_steps - t - 1);
+        if (t + 1 < n_steps) balance_prio(bal_row, bal_slot, bal_r0, t + 1, n_steps - t - 1);
 #endif
 #ifdef HFTLOB_STAMPS
         // rollout-only phases beside env_step_dev's stamps: the step-key batch (every KB_STEPS-th
@@ -3142,12 +3154,9 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
 #endif
     }
 #ifndef HFTLOB_NO_BALANCE
-    {  // the wave is done: its slot's entry becomes a past time, so no neighbour counts it as live
-        u32 slot;
-        unsigned long long* row = wave_row(bal_hwid, bal_xcc, slot);
-        if (lane_id() == 0) __hip_atomic_store(row + slot, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // the wave is done: its slot's entry becomes a past time, so no neighbour counts it as live
+    if (lane_id() == 0) __hip_atomic_store(bal_row + bal_slot, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
 #endif
     if ((e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
 }
@@ -3302,6 +3311,7 @@ static int check_env(const hftlob_env_cfg* c) {
     if (c->n_data_msg < 1 || c->n_data_rows < c->n_data_msg || c->n_windows < 1)
         return fail(HFTLOB_ESHAPE, "data / window sizes out of range");
     if (c->obs_stride > HFTLOB_MAX_OBS) return fail(HFTLOB_ESHAPE, "obs_stride too large");
+    if (c->tick_size < 1) return fail(HFTLOB_EINVAL, "tick_size must be >= 1");
     int agents = 0;
     for (int t = 0; t < c->n_types; ++t) {
         const hftlob_agent_type_cfg& tc = c->types[t];
@@ -3338,6 +3348,15 @@ static int check_env(const hftlob_env_cfg* c) {
     return HFTLOB_OK;
 }
 
+// the kernels' copy of the config: tick_magic for tick_floordiv (a caller's value is ignored)
+static hftlob_env_cfg kernel_cfg(const hftlob_env_cfg* cfg) {
+    hftlob_env_cfg c = *cfg;
+    const uint32_t d = (uint32_t)c.tick_size;  // >= 1 (check_env)
+    const int l = d > 1u ? 32 - __builtin_clz(d - 1u) : 0;
+    c.tick_magic = (uint32_t)((((unsigned __int128)1 << (31 + l)) + d - 1u) / d);
+    return c;
+}
+
 int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys, const int32_t* msg_data,
                      const int32_t* init_states, int32_t* state, const hftlob_step_out* out, void* stream) {
     int rc = check_env(cfg);
@@ -3350,9 +3369,10 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
-    if (S == 1) hipLaunchKernelGGL(k_env_reset<1>, g, b, 0, st, *cfg, n_env, keys, init_states, state, obs);
-    else if (S == 2) hipLaunchKernelGGL(k_env_reset<2>, g, b, 0, st, *cfg, n_env, keys, init_states, state, obs);
-    else hipLaunchKernelGGL(k_env_reset<4>, g, b, 0, st, *cfg, n_env, keys, init_states, state, obs);
+    const hftlob_env_cfg kc = kernel_cfg(cfg);
+    if (S == 1) hipLaunchKernelGGL(k_env_reset<1>, g, b, 0, st, kc, n_env, keys, init_states, state, obs);
+    else if (S == 2) hipLaunchKernelGGL(k_env_reset<2>, g, b, 0, st, kc, n_env, keys, init_states, state, obs);
+    else hipLaunchKernelGGL(k_env_reset<4>, g, b, 0, st, kc, n_env, keys, init_states, state, obs);
     return launch_status();
 }
 
@@ -3375,7 +3395,8 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
     const size_t shm = env_shm(cfg);
-#define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, keys, \
+    const hftlob_env_cfg kc = kernel_cfg(cfg);
+#define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, kc, n_env, key_e0, key_n, keys, \
                                                key_in, key_out, actions, msg_data, init_states, state, *out)
     if (cfg->lob.cancel_mode >= 2) {  // random cancel fallback: general sizes only
         if (S == 1) LAUNCH_STEP(1, 0, true);
@@ -3399,7 +3420,8 @@ static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, 
     hipStream_t st = (hipStream_t)stream;
     dim3 g(n_env), b(64);
     const size_t shm = env_shm(cfg);
-#define LAUNCH_ROLL(SS, NF, RC) hipLaunchKernelGGL((k_env_rollout<SS, NF, RC>), g, b, shm, st, *cfg, n_env, key_e0, key_n, \
+    const hftlob_env_cfg kc = kernel_cfg(cfg);
+#define LAUNCH_ROLL(SS, NF, RC) hipLaunchKernelGGL((k_env_rollout<SS, NF, RC>), g, b, shm, st, kc, n_env, key_e0, key_n, \
                                                n_steps, per_step, key_in, key_out, actions, msg_data, init_states, \
                                                state, *out)
     if (cfg->lob.cancel_mode >= 2) {

@@ -65,7 +65,7 @@ class EnvCfg(C.Structure):
         "shuffle_action_messages", "prng_partitionable", "n_types", "n_agents", "obs_stride",
         "rec_words", "init_rec_words", "off_asks", "off_bids", "off_trades", "off_loaded",
         "off_best_bids", "off_best_asks", "off_world", "off_agents", "info_words")] + [
-        ("action_words", C.c_int32), ("_pad", C.c_int32 * 1), ("types", AgentTypeCfg * MAX_TYPES)]
+        ("action_words", C.c_int32), ("tick_magic", C.c_uint32), ("types", AgentTypeCfg * MAX_TYPES)]
 
 
 class StepOut(C.Structure):

@@ -199,6 +199,12 @@ void oracle_permutation(const u32* key, int n, int part, int* perm) {
 #ifdef ORACLE_STATS /* message-mix statistics (tools/msg_mix.py; single-threaded builds only) */
 long long oracle_stats[32];
 #define STAT(i) (oracle_stats[i]++)
+/* per-message class trace (tools/msg_runs.py): 0 doNothing, 1 add behind / at the best, 2 add
+ * improving the best, 3 crossing add, 4 add into a full side, 5 cancel of quantity 0, 6 cancel
+ * found by id, 7 cancel found by the init-id fallback, 8 cancel of no row into an empty last
+ * slot, 9 cancel of no row into an occupied last slot */
+signed char oracle_trace[1 << 24];
+long long oracle_trace_n;
 #else
 #define STAT(i) ((void)0)
 #endif
@@ -455,6 +461,29 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
     i32 ba0[2], bb0[2], ba1[2], bb1[2];
     best_quotes(c, asks, bids, ba0, bb0);
 #endif
+    int cls = -1;
+    if (index == 4) cls = 0;
+    else if (index >= 2) {
+        const i32* sd = index == 2 ? asks : bids;
+        int nO = c->n_orders, idx = -1;
+        for (int i = 0; i < nO; ++i)
+            if (sd[i * 6 + 2] == m.oid) { idx = i; break; }
+        if (m.qty == 0) cls = 5;
+        else if (idx >= 0) cls = 6;
+        else {
+            i32 lo = wsub(c->init_id, wmul(c->book_depth, 2));
+            for (int i = 0; i < nO; ++i) {
+                const i32* r = sd + i * 6;
+                if (r[0] == m.price && r[2] <= c->init_id && r[2] >= lo && r[1] >= m.qty) { idx = i; break; }
+            }
+            cls = idx >= 0 ? 7 : (sd[(nO - 1) * 6] == -1 ? 8 : 9);
+        }
+    } else {
+        const i32* own = index == 1 ? bids : asks;
+        int nO = c->n_orders, full = 1;
+        for (int i = 0; i < nO; ++i) full &= own[i * 6] >= 0;
+        cls = full ? 4 : 1;
+    }
     switch (index) {
         case 0: ask_lim(c, m, asks, bids, trades); break;
         case 1: bid_lim(c, m, asks, bids, trades); break;
@@ -465,6 +494,9 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
 #ifdef ORACLE_STATS
     if ((index == 0 || index == 1) && oracle_stats[20] > before) STAT(7);   /* crossing */
     best_quotes(c, asks, bids, ba1, bb1);
+    if (cls == 1 && oracle_stats[20] > before) cls = 3;
+    else if (cls == 1 && (index == 1 ? bb1[0] != bb0[0] : ba1[0] != ba0[0])) cls = 2;
+    if (oracle_trace_n < (1 << 24)) oracle_trace[oracle_trace_n++] = (signed char)cls;
     if (ba1[0] != ba0[0]) STAT(15);
     if (bb1[0] != bb0[0]) STAT(16);
     if (ba1[0] != ba0[0] || ba1[1] != ba0[1]) STAT(17);

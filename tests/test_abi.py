@@ -125,6 +125,7 @@ def test_error_bad_env_cfg(L):
     for mutate, code in ((lambda c: setattr(c, "ep_type", 2), -1),
                          (lambda c: setattr(c, "n_agents", 3), -1),
                          (lambda c: setattr(c, "n_msgs", 1000), -3),
+                         (lambda c: setattr(c, "tick_size", 0), -1),      # tick_floordiv needs a tick >= 1
                          (lambda c: setattr(c.types[0], "kind", 7), -1),
                          (lambda c: setattr(c, "action_words", 3), -1),
                          (lambda c: setattr(c.types[0], "action_width", 2), -1),

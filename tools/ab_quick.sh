@@ -8,7 +8,7 @@ O=$GRAFT_REPO_ROOT/gpurun_out/$T
 mkdir -p $O
 cd $GRAFT_REPO_ROOT
 LIBS="base $(cd ab && ls lib_*.so 2>/dev/null | sed 's/\.so$//')"
-for r in 1 2 3; do
+for r in $(seq 1 ${ROUNDS:-3}); do
   for L in $LIBS; do
     if [ "$L" = base ]; then unset HFTLOB_LIB; else export HFTLOB_LIB=$GRAFT_REPO_ROOT/ab/$L.so; fi
     timeout -k 10 120 python bench.py --no-cpu-baseline > $O/b128_${L}_$r.json 2>> $O/bench.err || exit 3
@@ -17,11 +17,11 @@ for r in 1 2 3; do
 done
 unset HFTLOB_LIB
 for L in $LIBS; do
-  python - "$O" "$L" <<'PY'
+  python - "$O" "$L" "${ROUNDS:-3}" <<'PY'
 import json, sys
-O, L = sys.argv[1], sys.argv[2]
+O, L, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
 v = lambda k, r: json.load(open(f"{O}/{k}_{L}_{r}.json"))["value"] / 1e6
-print(f"{L:16s} 128 steps: " + " ".join(f"{v('b128', r):.2f}" for r in (1, 2, 3)) +
-      "   20 steps: " + " ".join(f"{v('b20', r):.2f}" for r in (1, 2, 3)))
+print(f"{L:16s} 128 steps: " + " ".join(f"{v('b128', r):.2f}" for r in range(1, n + 1)) +
+      "   20 steps: " + " ".join(f"{v('b20', r):.2f}" for r in range(1, n + 1)))
 PY
 done > $O/summary.txt 2>&1
