@@ -1403,6 +1403,9 @@ template <int S> DEV void global_pq(const i32* g, const Valid<S>& V, i32 (&p)[S]
 }
 
 // canonical float sum of per-row values over n rows held S-strided
+// rows_fsum of n rows that all hold the same signed zero z: z when every lane sums rows (n >= 64),
+// +0 otherwise (the lanes past n add +0)
+DEV float zsum(float z, int n) { return n >= 64 ? z : z + 0.0f; }
 template <int S> DEV float rows_fsum(const float (&x)[S], int n) {
     const int l = lane_id();
     float a = l < n ? x[0] : 0.0f;
@@ -1411,19 +1414,23 @@ template <int S> DEV float rows_fsum(const float (&x)[S], int n) {
     return wave_fsum(a);
 }
 
-// One agent's observation row, one field per lane: `o[k] = x` keeps x in lane k.  (The obs
-// functions fill fields by config-dependent branches; a local float array written that way
-// ends up in scratch memory, with a scratch store per field per lane.)
+// One agent's observation row, one field per lane: put(k, x, off, div) keeps field k's raw value x
+// and its normalisation (x - off) / div (normalize_obs, mm_env.py:3157-3167: (x - mean) / std) in
+// lane k, and fin() divides once for all fields (one vector division instead of one per field;
+// the same IEEE operations per field: x - 0 == x and x / 1 == x exactly).  (The obs functions
+// fill fields by config-dependent branches; a local float array written that way ends up in
+// scratch memory, with a scratch store per field per lane.)
 struct ObsLane {
     int l;
-    float v;
-    struct Ref {
-        ObsLane& o;
-        int k;
-        DEV void operator=(float x) { o.v = o.l == k ? x : o.v; }
-    };
-    DEV Ref operator[](int k) { return Ref{*this, k}; }
+    float v = 0.0f, off = 0.0f, div = 1.0f;
+    DEV void put(int k, float x, float o, float d) {
+        const bool me = l == k;
+        v = me ? x : v;
+        off = me ? o : off;
+        div = me ? d : div;
+    }
     DEV void put_i(int k, i32 x) { v = l == k ? __int_as_float(x) : v; }  // an int32 field, kept as its bits
+    DEV float fin() const { return (v - off) / div; }
 };
 
 struct WorldView {  // wave-uniform world quantities used by obs
@@ -1438,15 +1445,17 @@ struct WorldView {  // wave-uniform world quantities used by obs
 // RAW: get_observation(normalize=False, flatten=False) for save_raw_observations
 // (marl_env.py:684-685): no normalisation, and the int32 fields keep their int32
 // value (stored as int bits; flattening is what casts them to float).
-#define OBS_I(k, x, expr) do { if (RAW) o.put_i((k), (x)); else o[k] = (expr); } while (0)
+// OBS_F: a float field x, normalised (x - o) / d; OBS_I: an int32 field x, as float i2f(x)
+#define OBS_F(k, x, o_, d_) o.put((k), (x), nz ? (o_) : 0.0f, nz ? (d_) : 1.0f)
+#define OBS_I(k, x, o_, d_) do { if (RAW) o.put_i((k), (x)); else OBS_F((k), i2f(x), (o_), (d_)); } while (0)
 template <bool RAW>
 DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st, ObsLane& o,
                 bool ftime) {
     const bool nz = !RAW && tc.normalize;
     const i32 spread = iabs_(wsub(w.best_ask_p, w.best_bid_p));
     if (tc.observation_space == HFTLOB_MM_OBS_BASIC) {  // inventory, spread
-        OBS_I(0, st[2], nz ? i2f(st[2]) / 10.0f : i2f(st[2]));
-        OBS_I(1, spread, nz ? i2f(spread) / 1e4f : i2f(spread));
+        OBS_I(0, st[2], 0.0f, 10.0f);
+        OBS_I(1, spread, 0.0f, 1e4f);
         return;
     }
     // "messages" (mm_env.py:2820-2821): the observation is the step's message array, written
@@ -1456,27 +1465,27 @@ DEV void mm_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const 
                   // q_bid, spread, step_counter, time_remaining
         const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
         const float trem = (float)c.episode_time - (tm - (i2f(w.it0) + i2f(w.it1) / 1e9f));
-        o[0] = nz ? w.dt / 10.0f : w.dt;
-        OBS_I(1, st[2], nz ? i2f(st[2]) / 10.0f : i2f(st[2]));
-        o[2] = nz ? w.mid / 1e6f : w.mid;
-        OBS_I(3, w.best_ask_p, nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p));
-        OBS_I(4, w.best_bid_p, nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p));
-        OBS_I(5, w.vol_a, nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a));
-        OBS_I(6, w.vol_b, nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b));
-        OBS_I(7, spread, nz ? i2f(spread) / 1e4f : i2f(spread));
-        OBS_I(8, w.step, nz ? i2f(w.step) / 10.0f : i2f(w.step));
-        o[9] = nz ? trem / (float)c.episode_time : trem;
+        OBS_F(0, w.dt, 0.0f, 10.0f);
+        OBS_I(1, st[2], 0.0f, 10.0f);
+        OBS_F(2, w.mid, 0.0f, 1e6f);
+        OBS_I(3, w.best_ask_p, 0.0f, 1e6f);
+        OBS_I(4, w.best_bid_p, 0.0f, 1e6f);
+        OBS_I(5, w.vol_a, 0.0f, 1000.0f);
+        OBS_I(6, w.vol_b, 0.0f, 1000.0f);
+        OBS_I(7, spread, 0.0f, 1e4f);
+        OBS_I(8, w.step, 0.0f, 10.0f);
+        OBS_F(9, trem, 0.0f, (float)c.episode_time);
         return;
     }
     // fixed_steps: inventory, mid_price, p_ask, p_bid, q_ask, q_bid, spread, step_counter
-    OBS_I(0, st[2], nz ? i2f(st[2]) / 10.0f : i2f(st[2]));
-    o[1] = nz ? w.mid / 1e6f : w.mid;
-    OBS_I(2, w.best_ask_p, nz ? i2f(w.best_ask_p) / 1e6f : i2f(w.best_ask_p));
-    OBS_I(3, w.best_bid_p, nz ? i2f(w.best_bid_p) / 1e6f : i2f(w.best_bid_p));
-    OBS_I(4, w.vol_a, nz ? i2f(w.vol_a) / 1000.0f : i2f(w.vol_a));
-    OBS_I(5, w.vol_b, nz ? i2f(w.vol_b) / 1000.0f : i2f(w.vol_b));
-    OBS_I(6, spread, nz ? i2f(spread) / 1e4f : i2f(spread));
-    OBS_I(7, w.step, nz ? i2f(w.step) / 10.0f : i2f(w.step));
+    OBS_I(0, st[2], 0.0f, 10.0f);
+    OBS_F(1, w.mid, 0.0f, 1e6f);
+    OBS_I(2, w.best_ask_p, 0.0f, 1e6f);
+    OBS_I(3, w.best_bid_p, 0.0f, 1e6f);
+    OBS_I(4, w.vol_a, 0.0f, 1000.0f);
+    OBS_I(5, w.vol_b, 0.0f, 1000.0f);
+    OBS_I(6, spread, 0.0f, 1e4f);
+    OBS_I(7, w.step, 0.0f, 10.0f);
 }
 // EXE _get_obs / _get_obs_basic / _get_obs_simplest_case, sorted keys — exec_env.py:1841-2079
 // ftime: ep_type == fixed_time, passed by the caller (compile-time false in the 100/100 kernel)
@@ -1485,10 +1494,16 @@ DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
                  bool ftime) {
     const bool nz = !RAW && tc.normalize;
     if (tc.observation_space == HFTLOB_EXE_OBS_BASIC) {  // :1879-1911 best_ask_price, best_bid_price, remaining_quant
+        // (normalised: the int32 price minus 1550000, then / 1e3)
         const i32 rq = wsub(st[1], st[2]);
-        OBS_I(0, w.best_ask_p, nz ? i2f(wsub(w.best_ask_p, 1550000)) / 1e3f : i2f(w.best_ask_p));
-        OBS_I(1, w.best_bid_p, nz ? i2f(wsub(w.best_bid_p, 1550000)) / 1e3f : i2f(w.best_bid_p));
-        OBS_I(2, rq, nz ? i2f(rq) / (float)tc.task_size : i2f(rq));
+        if (RAW) {
+            o.put_i(0, w.best_ask_p);
+            o.put_i(1, w.best_bid_p);
+        } else {
+            o.put(0, i2f(nz ? wsub(w.best_ask_p, 1550000) : w.best_ask_p), 0.0f, nz ? 1e3f : 1.0f);
+            o.put(1, i2f(nz ? wsub(w.best_bid_p, 1550000) : w.best_bid_p), 0.0f, nz ? 1e3f : 1.0f);
+        }
+        OBS_I(2, rq, 0.0f, (float)tc.task_size);
         return;
     }
     if (tc.observation_space == HFTLOB_EXE_OBS_SIMPLEST_CASE) {
@@ -1496,9 +1511,9 @@ DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
         const float ep = (float)c.episode_time;
         const float ptr = (ep - (i2f(wsub(w.t0, w.it0)) + i2f(wsub(w.t1, w.it1)) / 1e9f)) / ep;
         const float prq = i2f(wsub(st[1], st[2])) / i2f(st[1]);
-        o[0] = nz ? (w.mid - 7560000.0f) / 1e3f : w.mid;
-        o[1] = nz ? (prq - 0.5f) / 1.0f : prq;
-        o[2] = nz ? (ptr - 0.5f) / 1.0f : ptr;
+        OBS_F(0, w.mid, 7560000.0f, 1e3f);
+        OBS_F(1, prq, 0.5f, 1.0f);
+        OBS_F(2, ptr, 0.5f, 1.0f);
         return;
     }
     const i32 sell = st[3];
@@ -1513,41 +1528,42 @@ DEV void exe_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
         // fixed_time (exec_env.py:1940-2010): 15 keys, sorted: delta_time, executed_quant, init_price,
         // is_sell_task, p_aggr, p_pass, q_aggr, q_pass, remaining_quant, remaining_ratio, spread,
         // step_counter, task_size, time, time_remaining
-        o[0] = nz ? w.dt / 10.0f : w.dt;
+        OBS_F(0, w.dt, 0.0f, 10.0f);
         k = 1;
     }
     // fixed_steps (12 keys): executed_quant, init_price, is_sell_task, p_aggr, p_pass, q_aggr, q_pass,
     // remaining_quant, remaining_ratio, spread, step_counter, task_size
-    OBS_I(k + 0, st[2], nz ? i2f(st[2]) / ts : i2f(st[2]));
-    o[k + 1] = nz ? ip / 1e7f : ip;
-    OBS_I(k + 2, sell, nz ? i2f(sell) / 1.0f : i2f(sell));
-    OBS_I(k + 3, p_aggr, nz ? (i2f(p_aggr) - ip) / 1e5f : i2f(p_aggr));
-    OBS_I(k + 4, p_pass, nz ? (i2f(p_pass) - ip) / 1e5f : i2f(p_pass));
-    OBS_I(k + 5, q_aggr, nz ? i2f(q_aggr) / 1000.0f : i2f(q_aggr));
-    OBS_I(k + 6, q_pass, nz ? i2f(q_pass) / 1000.0f : i2f(q_pass));
-    OBS_I(k + 7, rq, nz ? i2f(rq) / ts : i2f(rq));
-    o[k + 8] = nz ? rr / 1.0f : rr;
-    OBS_I(k + 9, spr, nz ? i2f(spr) / 1e4f : i2f(spr));
-    OBS_I(k + 10, w.step, nz ? i2f(w.step) / 30.0f : i2f(w.step));
-    OBS_I(k + 11, st[1], nz ? i2f(st[1]) / ts : i2f(st[1]));
+    OBS_I(k + 0, st[2], 0.0f, ts);
+    OBS_F(k + 1, ip, 0.0f, 1e7f);
+    OBS_I(k + 2, sell, 0.0f, 1.0f);
+    OBS_I(k + 3, p_aggr, ip, 1e5f);
+    OBS_I(k + 4, p_pass, ip, 1e5f);
+    OBS_I(k + 5, q_aggr, 0.0f, 1000.0f);
+    OBS_I(k + 6, q_pass, 0.0f, 1000.0f);
+    OBS_I(k + 7, rq, 0.0f, ts);
+    OBS_F(k + 8, rr, 0.0f, 1.0f);
+    OBS_I(k + 9, spr, 0.0f, 1e4f);
+    OBS_I(k + 10, w.step, 0.0f, 30.0f);
+    OBS_I(k + 11, st[1], 0.0f, ts);
     if (ftime) {
         const float tm = i2f(w.t0) + i2f(w.t1) / 1e9f;
         const float trem = (float)c.episode_time - (tm - (i2f(w.it0) + i2f(w.it1) / 1e9f));
-        o[13] = nz ? tm / 1e5f : tm;
-        o[14] = nz ? trem / (float)c.episode_time : trem;
+        OBS_F(13, tm, 0.0f, 1e5f);
+        OBS_F(14, trem, 0.0f, (float)c.episode_time);
     }
 }
 #undef OBS_I
+#undef OBS_F
 // write one agent's obs row (lanes 0..obs_stride-1 store one 32-bit word each);
 // RAW: the un-normalised row of obs_raw
 template <bool RAW>
 DEV void write_obs(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const WorldView& w, const i32* st,
                    void* dst, bool zero, bool ftime) {
     const int l = lane_id();
-    ObsLane o{l, 0.0f};
+    ObsLane o{l};
     if (tc.kind == HFTLOB_AGENT_MM) mm_obs<RAW>(c, tc, w, st, o, ftime);
     else exe_obs<RAW>(c, tc, w, st, o, ftime);
-    const float v = zero ? 0.0f : o.v;
+    const float v = zero ? 0.0f : (RAW ? o.v : o.fin());
     if (l < c.obs_stride) static_cast<float*>(dst)[l] = v;
 }
 
@@ -2109,29 +2125,50 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     const int ri = tc.reference_price;
     const bool ref_int = ri == HFTLOB_PRICE_FAR_TOUCH || ri == HFTLOB_PRICE_NEAR_TOUCH;
     i32 bq = 0, sq = 0, oq = 0;
-    float inc[S], out[S], rb[S], rsl[S];
     i32 bP[S], bQ[S], sP[S], sQ[S];
+    float income, outgoing, rebate_value;
+    lmask anym = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) {
-        const bool mine = (tid == V.PT[r]) || (tid == V.AT[r]);
-        const i32 aP = mine ? V.P[r] : 0, aQ = mine ? V.Q[r] : 0, apt = mine ? V.PT[r] : 0, aat = mine ? V.AT[r] : 0;
-        oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
-        const bool buy = (aQ >= 0 && tid == apt) || (aQ < 0 && tid == aat);
-        const bool sel = (aQ < 0 && tid == apt) || (aQ >= 0 && tid == aat);
-        const bool pbuy = (aQ >= 0 && tid == apt), psel = (aQ < 0 && tid == apt);
-        bP[r] = buy ? aP : 0; bQ[r] = buy ? aQ : 0; sP[r] = sel ? aP : 0; sQ[r] = sel ? aQ : 0;
-        const i32 pbP = pbuy ? aP : 0, pbQ = pbuy ? aQ : 0, psP = psel ? aP : 0, psQ = psel ? aQ : 0;
-        bq = wadd(bq, iabs_(bQ[r]));
-        sq = wadd(sq, iabs_(sQ[r]));
-        inc[r] = i2f(sP[r]) / tick * i2f(iabs_(sQ[r]));
-        out[r] = i2f(bP[r]) / tick * i2f(iabs_(bQ[r]));
-        rb[r] = i2f(pbP) / tick * i2f(iabs_(pbQ));
-        rsl[r] = i2f(psP) / tick * i2f(iabs_(psQ));
+    for (int r = 0; r < S; ++r) anym |= bal((tid == V.PT[r]) || (tid == V.AT[r]));
+    const bool quiet = anym == 0ull;
+    if (quiet) {
+        // no row is the agent's (no fill this step: 98 % of the metric's steps): every buy / sell
+        // stat is 0 and every float row term below is one and the same signed zero, summed by
+        // zsum exactly as rows_fsum would
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            oq = wadd(oq, iabs_(V.Q[r]));
+            bP[r] = bQ[r] = sP[r] = sQ[r] = 0;
+        }
+        oq = wave_sum(oq);
+        const float z = i2f(0) / tick * i2f(0);
+        income = outgoing = zsum(z, nT);
+        rebate_value = zsum(z, nT) + zsum(z, nT);
+    } else {
+        float inc[S], out[S], rb[S], rsl[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const bool mine = (tid == V.PT[r]) || (tid == V.AT[r]);
+            const i32 aP = mine ? V.P[r] : 0, aQ = mine ? V.Q[r] : 0, apt = mine ? V.PT[r] : 0, aat = mine ? V.AT[r] : 0;
+            oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
+            const bool buy = (aQ >= 0 && tid == apt) || (aQ < 0 && tid == aat);
+            const bool sel = (aQ < 0 && tid == apt) || (aQ >= 0 && tid == aat);
+            const bool pbuy = (aQ >= 0 && tid == apt), psel = (aQ < 0 && tid == apt);
+            bP[r] = buy ? aP : 0; bQ[r] = buy ? aQ : 0; sP[r] = sel ? aP : 0; sQ[r] = sel ? aQ : 0;
+            const i32 pbP = pbuy ? aP : 0, pbQ = pbuy ? aQ : 0, psP = psel ? aP : 0, psQ = psel ? aQ : 0;
+            bq = wadd(bq, iabs_(bQ[r]));
+            sq = wadd(sq, iabs_(sQ[r]));
+            inc[r] = i2f(sP[r]) / tick * i2f(iabs_(sQ[r]));
+            out[r] = i2f(bP[r]) / tick * i2f(iabs_(bQ[r]));
+            rb[r] = i2f(pbP) / tick * i2f(iabs_(pbQ));
+            rsl[r] = i2f(psP) / tick * i2f(iabs_(psQ));
+        }
+        bq = wave_sum(bq); sq = wave_sum(sq); oq = wave_sum(oq);
+        income = rows_fsum(inc, nT);
+        outgoing = rows_fsum(out, nT);
+        rebate_value = rows_fsum(rb, nT) + rows_fsum(rsl, nT);
     }
-    bq = wave_sum(bq); sq = wave_sum(sq); oq = wave_sum(oq);
-    const float income = rows_fsum(inc, nT), outgoing = rows_fsum(out, nT);
     const i32 new_inv = wsub(wadd(inv, bq), sq);
-    const float rebate_value = rows_fsum(rb, nT) + rows_fsum(rsl, nT);
     const float rebate_income = rebate_value * tc.rebate_factor;
     float ref_buy, ref_sell, ref;
     i32 rbi = 0, rsi = 0, refi = 0;
@@ -2151,18 +2188,27 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     const float market_share = i2f(traded) / i2f(wadd(traded, oq));
     const float mid_end = X.last_mid;
     const float invPnL = i2f(inv) * (mid_end - X.wmid) / tick;
-    float bpl[S], spl[S];
+    float buyPnL, sellPnL;
+    if (quiet) {  // (the rows' one signed zero: sign of the reference price term)
+        const float zb = ref_int ? i2f(wsub(rbi, 0)) / tick * i2f(0) : (ref_buy - i2f(0)) / tick * i2f(0);
+        const float zs = ref_int ? i2f(wsub(0, rsi)) / tick * i2f(0) : (i2f(0) - ref_sell) / tick * i2f(0);
+        buyPnL = zsum(zb, nT);
+        sellPnL = zsum(zs, nT);
+    } else {
+        float bpl[S], spl[S];
 #pragma unroll
-    for (int r = 0; r < S; ++r) {
-        if (ref_int) {
-            bpl[r] = i2f(wsub(rbi, bP[r])) / tick * i2f(iabs_(bQ[r]));
-            spl[r] = i2f(wsub(sP[r], rsi)) / tick * i2f(iabs_(sQ[r]));
-        } else {
-            bpl[r] = (ref_buy - i2f(bP[r])) / tick * i2f(iabs_(bQ[r]));
-            spl[r] = (i2f(sP[r]) - ref_sell) / tick * i2f(iabs_(sQ[r]));
+        for (int r = 0; r < S; ++r) {
+            if (ref_int) {
+                bpl[r] = i2f(wsub(rbi, bP[r])) / tick * i2f(iabs_(bQ[r]));
+                spl[r] = i2f(wsub(sP[r], rsi)) / tick * i2f(iabs_(sQ[r]));
+            } else {
+                bpl[r] = (ref_buy - i2f(bP[r])) / tick * i2f(iabs_(bQ[r]));
+                spl[r] = (i2f(sP[r]) - ref_sell) / tick * i2f(iabs_(sQ[r]));
+            }
         }
+        buyPnL = rows_fsum(bpl, nT);
+        sellPnL = rows_fsum(spl, nT);
     }
-    const float buyPnL = rows_fsum(bpl, nT), sellPnL = rows_fsum(spl, nT);
     const float eta = tc.inventoryPnL_eta, gam = tc.inventoryPnL_gamma;
     const float r_sp = buyPnL + sellPnL + rebate_income + invPnL;
     const float r_spd = buyPnL + sellPnL + rebate_income + invPnL - eta * invPnL;
@@ -2273,17 +2319,29 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
         R.doom_quant = quant_left;
     }
     i32 aq = 0, oq = 0, qp = 0;
-    float dur[S];
+    lmask anym = 0;
 #pragma unroll
-    for (int r = 0; r < S; ++r) {
-        const bool mine = V.valid[r] && (tid == V.PT[r] || tid == V.AT[r]);
-        aq = wadd(aq, mine ? iabs_(V.Q[r]) : 0);
-        oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
-        qp = wadd(qp, mine ? wmul(tick_floordiv(c, V.P[r]), iabs_(V.Q[r])) : 0);
-        dur[r] = mine ? i2f(iabs_(V.Q[r])) / i2f(task) * i2f(wsub(V.S4[r], X.init0))
-                      : i2f(0) / i2f(task) * i2f(wsub(0, X.init0));
+    for (int r = 0; r < S; ++r) anym |= bal(V.valid[r] && (tid == V.PT[r] || tid == V.AT[r]));
+    float dur_sum;
+    if (anym == 0ull) {  // no fill of the agent this step: aq = qp = 0, every duration term the same signed zero
+#pragma unroll
+        for (int r = 0; r < S; ++r) oq = wadd(oq, iabs_(V.Q[r]));
+        oq = wave_sum(oq);
+        dur_sum = zsum(i2f(0) / i2f(task) * i2f(wsub(0, X.init0)), nT);
+    } else {
+        float dur[S];
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            const bool mine = V.valid[r] && (tid == V.PT[r] || tid == V.AT[r]);
+            aq = wadd(aq, mine ? iabs_(V.Q[r]) : 0);
+            oq = wadd(oq, mine ? 0 : iabs_(V.Q[r]));
+            qp = wadd(qp, mine ? wmul(tick_floordiv(c, V.P[r]), iabs_(V.Q[r])) : 0);
+            dur[r] = mine ? i2f(iabs_(V.Q[r])) / i2f(task) * i2f(wsub(V.S4[r], X.init0))
+                          : i2f(0) / i2f(task) * i2f(wsub(0, X.init0));
+        }
+        aq = wave_sum(aq); oq = wave_sum(oq); qp = wave_sum(qp);
+        dur_sum = rows_fsum(dur, nT);
     }
-    aq = wave_sum(aq); oq = wave_sum(oq); qp = wave_sum(qp);
     float pv;
     if (oq == 0) pv = ffloordiv(X.avg_mid, (float)tick);
     else {
@@ -2308,7 +2366,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     R.slippage_rm = (bitf(st[8]) * scf + slip) / sc1;
     R.price_drift_rm = (bitf(st[10]) * scf + pdrift) / sc1;
     float reward = adv + tc.reward_lambda * drift;
-    R.trade_duration = bitf(st[12]) + rows_fsum(dur, nT);
+    R.trade_duration = bitf(st[12]) + dur_sum;
     R.quant_left = wsub(wsub(task, qe), aq);
     R.reward_info = reward;
     if (tc.reward_function == HFTLOB_EXE_REW_FINISH_FAST) reward = i2f(wsub(0, iabs_(R.quant_left)));
@@ -2746,10 +2804,12 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     for (int k = 0; k < 6; ++k) if (l == k) v = xv[k];
                     if (l < 6) axs[ag * 6 + l] = v;
                 }
+#ifndef HFTLOB_KO_FILTER  // timing knockout builds only (wrong results)
                 if (tc.n_action_msgs == 2) filter_rows<2>(rows, arow, crow, B.a.scr);
                 else if (tc.n_action_msgs == 4) filter_rows<4>(rows, arow, crow, B.a.scr);
                 else if (NFIX == 0 && tc.n_action_msgs == 3) filter_rows<3>(rows, arow, crow, B.a.scr);  // fixed_prices
                 else filter_rows<1>(rows, arow, crow, B.a.scr);
+#endif
                 STAMP_ACC(acc_flt, ta2);
                 arow += tc.n_action_msgs;
                 crow += tc.n_msgs - tc.n_action_msgs;
@@ -2901,7 +2961,11 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 STAMP(tr0);
                 if (tc.kind == HFTLOB_AGENT_MM) {
                     MMRew R;
+#ifdef HFTLOB_KO_REWARD  // timing knockout builds only (wrong results)
+                    memset(&R, 0, sizeof R);
+#else
                     mm_reward(c, tc, B, X, s, tid, excl_any, R);
+#endif
                     STAMP_ACC(acc_mmr, tr0);
                     const float tot = bitf(s[3]) + R.PnL;
                     s[0] = ax1.bid_dist; s[1] = ax1.ask_dist; s[2] = R.end_inventory; s[3] = fbit(tot);
@@ -2918,7 +2982,11 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     iw[23] = fbit(R.inventoryValue);
                 } else {
                     EXRew R;
+#ifdef HFTLOB_KO_REWARD
+                    memset(&R, 0, sizeof R);
+#else
                     exe_reward(c, tc, B, X, s, tid, R);
+#endif
                     STAMP_ACC(acc_exr, tr0);
                     s[2] = wadd(s[2], R.agentQuant);
                     s[4] = fbit(R.p_vwap);
@@ -2947,7 +3015,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     i32 v = 0;
                     for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
                     if (l < nw) st[l] = v;
+#ifndef HFTLOB_KO_OBS  // timing knockout builds only (wrong results)
                     write_obs<false>(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0, ftime);
+#endif
                 }
                 if (obs_raw_out)  // the stepped state's raw obs, also on an episode's last step (info)
                     write_obs<true>(c, tc, wv, s, obs_raw_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, false,
