@@ -1403,6 +1403,20 @@ template <int S> DEV void global_pq(const i32* g, const Valid<S>& V, i32 (&p)[S]
 }
 
 // canonical float sum of per-row values over n rows held S-strided
+// Independent scalar float divisions of one agent's reward, evaluated together: division k's
+// operands in lane k, one vector division, results read back per lane (the same IEEE quotients as
+// k separate scalar divisions, with one division's latency instead of k in a chain)
+struct DivBatch {
+    int l;
+    float n = 0.0f, d = 1.0f, q = 0.0f;
+    DEV void add(int k, float num, float den) {
+        n = l == k ? num : n;
+        d = l == k ? den : d;
+    }
+    DEV void run() { q = n / d; }
+    DEV float get(int k) const { return unif_lane(q, k); }
+    DEV static float unif_lane(float v, int k) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k)); }
+};
 // rows_fsum of n rows that all hold the same signed zero z: z when every lane sums rows (n >= 64),
 // +0 otherwise (the lanes past n add +0)
 DEV float zsum(float z, int n) { return n >= 64 ? z : z + 0.0f; }
@@ -2084,12 +2098,10 @@ struct MMRew {
 // MM get_reward — mm_env.py:2214-2673
 template <int S>
 DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const Book<S>& B, const StepCtx& X,
-                   const i32* st, i32 tid, bool excl_any, MMRew& R) {
+                   const i32* st, i32 tid, bool excl_any, const TradeView<S>& TV, MMRew& R) {
     const int nT = c.lob.n_trades;
     const float tick = (float)c.tick_size;
-    const i32 ovr0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    TradeView<S> V;
-    trade_view(B, V, false, -1, ovr0);
+    TradeView<S> V = TV;  // the step's trades (the unwind below overrides one row of this agent's copy)
     const i32 inv = st[2];
     const i32 M = c.n_msgs;
     // the forced unwind exists only on an episode's last step: the pre-unwind inventory and the
@@ -2141,9 +2153,9 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
             bP[r] = bQ[r] = sP[r] = sQ[r] = 0;
         }
         oq = wave_sum(oq);
-        const float z = i2f(0) / tick * i2f(0);
-        income = outgoing = zsum(z, nT);
-        rebate_value = zsum(z, nT) + zsum(z, nT);
+        // (0 / tick * 0 = +0: tick >= 1)
+        income = outgoing = zsum(0.0f, nT);
+        rebate_value = zsum(0.0f, nT) + zsum(0.0f, nT);
     } else {
         float inc[S], out[S], rb[S], rsl[S];
 #pragma unroll
@@ -2182,16 +2194,28 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     } else { ref_buy = ref_sell = ref = X.last_mid; }
     const float PnL = income - outgoing + rebate_income;
     const float cash = bitf(st[4]) + PnL;
-    const float inv_value = ref_int ? i2f(wmul(new_inv, refi)) / tick : i2f(new_inv) * ref / tick;
-    const float net_worth = cash + inv_value;
     const i32 traded = wadd(bq, sq);
-    const float market_share = i2f(traded) / i2f(wadd(traded, oq));
     const float mid_end = X.last_mid;
-    const float invPnL = i2f(inv) * (mid_end - X.wmid) / tick;
+    float old_ref;
+    if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_ba, X.old_last_bb));
+    else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_bb, X.old_last_ba));
+    else old_ref = X.wmid;
+    DivBatch D{lane_id()};
+    D.add(0, ref_int ? i2f(wmul(new_inv, refi)) : i2f(new_inv) * ref, tick);  // inventoryValue
+    D.add(1, i2f(traded), i2f(wadd(traded, oq)));                              // market_share
+    D.add(2, i2f(inv) * (mid_end - X.wmid), tick);                             // InventoryPnL
+    D.add(3, ref, tick);                                                       // portfolio value's ref / tick
+    D.add(4, old_ref, tick);                                                   // the old net worth's
+    D.run();
+    const float inv_value = D.get(0);
+    const float net_worth = cash + inv_value;
+    const float market_share = D.get(1);
+    const float invPnL = D.get(2);
     float buyPnL, sellPnL;
     if (quiet) {  // (the rows' one signed zero: sign of the reference price term)
-        const float zb = ref_int ? i2f(wsub(rbi, 0)) / tick * i2f(0) : (ref_buy - i2f(0)) / tick * i2f(0);
-        const float zs = ref_int ? i2f(wsub(0, rsi)) / tick * i2f(0) : (i2f(0) - ref_sell) / tick * i2f(0);
+        // (x / tick * +0 is the zero of x's sign: x finite, tick >= 1, |x| >= 1 or x = +-0)
+        const float zb = copysignf(0.0f, ref_int ? i2f(wsub(rbi, 0)) : ref_buy - i2f(0));
+        const float zs = copysignf(0.0f, ref_int ? i2f(wsub(0, rsi)) : i2f(0) - ref_sell);
         buyPnL = zsum(zb, nT);
         sellPnL = zsum(zs, nT);
     } else {
@@ -2231,12 +2255,8 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
                                             : i2f(iabs_(inv_change)) * (avg_sell - X.avg_mid);
         r_complex = real_pnl + tc.unrealizedPnL_lambda * unreal + eta * fminf(invPnL, invPnL * eta);
     }
-    const float r_pv = i2f(new_inv) * (ref / tick) + cash;
-    float old_ref;
-    if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_ba, X.old_last_bb));
-    else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_bb, X.old_last_ba));
-    else old_ref = X.wmid;
-    const float old_nw = old_ref / tick * i2f(inv) + bitf(st[4]);
+    const float r_pv = i2f(new_inv) * D.get(3) + cash;
+    const float old_nw = D.get(4) * i2f(inv) + bitf(st[4]);
     const float d_nw = net_worth - old_nw;
     float reward;
     switch (tc.reward_function) {
@@ -2281,12 +2301,10 @@ struct EXRew {
 // EXE get_reward — exec_env.py:1511-1762
 template <int S>
 DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const Book<S>& B, const StepCtx& X,
-                    const i32* st, i32 tid, EXRew& R) {
+                    const i32* st, i32 tid, const TradeView<S>& TV, EXRew& R) {
     const int nT = c.lob.n_trades;
     const i32 tick = c.tick_size;
-    const i32 ovr0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    TradeView<S> V;
-    trade_view(B, V, false, -1, ovr0);
+    TradeView<S> V = TV;  // the step's trades (the doom trade below overrides one row of this agent's copy)
     const i32 task = st[1], qe = st[2], sell = st[3];
     const float init_price = bitf(st[0]);
     // the fictional doom trade exists only on an episode's last step: the pre-unwind quantity and
@@ -2357,14 +2375,23 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     const i32 dirs = isign(wsub(wmul(sell, 2), 1));
     const float adv = i2f(dirs) * (i2f(qp) - pv * i2f(aq));
     const float drift = i2f(wmul(dirs, aq)) * (pv - ffloordiv(init_price, (float)tick));
-    const float padv = adv / (i2f(aq) + 1e-9f);
-    const float pdrift = drift / (i2f(aq) + 1e-9f);
     const float slip = adv + drift;
     const float scf = i2f(X.step), sc1 = i2f(wadd(X.step, 1));
-    R.vwap_rm = (bitf(st[11]) * scf + pv) / sc1;
-    R.price_adv_rm = (bitf(st[9]) * scf + padv) / sc1;
-    R.slippage_rm = (bitf(st[8]) * scf + slip) / sc1;
-    R.price_drift_rm = (bitf(st[10]) * scf + pdrift) / sc1;
+    DivBatch D{lane_id()};  // the per-agent averages, then the rolling means (exec_env.py:1760-1762)
+    D.add(0, adv, i2f(aq) + 1e-9f);
+    D.add(1, drift, i2f(aq) + 1e-9f);
+    D.add(2, bitf(st[11]) * scf + pv, sc1);
+    D.add(3, bitf(st[8]) * scf + slip, sc1);
+    D.run();
+    const float padv = D.get(0), pdrift = D.get(1);
+    R.vwap_rm = D.get(2);
+    R.slippage_rm = D.get(3);
+    DivBatch D2{lane_id()};
+    D2.add(0, bitf(st[9]) * scf + padv, sc1);
+    D2.add(1, bitf(st[10]) * scf + pdrift, sc1);
+    D2.run();
+    R.price_adv_rm = D2.get(0);
+    R.price_drift_rm = D2.get(1);
     float reward = adv + tc.reward_lambda * drift;
     R.trade_duration = bitf(st[12]) + dur_sum;
     R.quant_left = wsub(wsub(task, qe), aq);
@@ -2512,6 +2539,31 @@ __host__ __device__ inline bool kb_ok(const hftlob_env_cfg& c) {  // (a step's r
            6 + c.n_agents + c.n_action_msgs <= 16;
 }
 __host__ __device__ inline int kb_words(const hftlob_env_cfg& c) { return 6 + c.n_agents + c.n_action_msgs; }
+// LDS carve-up of one env's workgroup (words): [agent rows (C+A)*8][action extras][book: asks 6nO,
+// bids 6nO, trades 8nT, pad 256][key batches].  When the agent rows all fall in the first message
+// chunk (C + A <= 64) and fit the trade log's rows (C + A <= nT), they can live IN the trade log
+// instead: it is free from the step's start until trades_fill, which then runs after chunk 0's
+// rows are read.  (Speed_test's [5,5] agents: 60 rows, 1.9 KB less per env, 16 envs per CU
+// instead of 14.)
+__host__ __device__ inline bool rows_in_trades(const hftlob_env_cfg& c, int nT) {
+    const int ar = c.n_cancel_msgs + c.n_action_msgs;
+    return ar <= 64 && ar <= nT;
+}
+struct LdsMap {
+    int rows, axs, book, kb, words;  // word offsets, total words
+};
+// alias: the rows-in-trades layout (a separate kernel instantiation, RA, launched only where it
+// raises the envs a CU holds: use_rows_alias; the other kernels keep the rows' own region at 0)
+__host__ __device__ inline LdsMap lds_map(const hftlob_env_cfg& c, int nO, int nT, bool alias) {
+    LdsMap m;
+    const int rw = alias ? 0 : (c.n_cancel_msgs + c.n_action_msgs) * 8;
+    m.axs = rw;
+    m.book = rw + ((c.n_agents * 6 + 3) & ~3);
+    m.rows = alias ? m.book + 12 * nO : 0;  // (the trade log)
+    m.kb = m.book + 12 * nO + 8 * nT + 256;
+    m.words = m.kb + (kb_ok(c) ? KB_STEPS * kb_words(c) : 0);
+    return m;
+}
 template <bool MD>
 DEV void step_keys_batch(const hftlob_env_cfg& c, int n_env, int e, Key& mk, int nb, i32* kb) {
     const bool part = true;
@@ -2565,7 +2617,7 @@ DEV StepKeys load_keys(const hftlob_env_cfg& c, const i32* row) {
     o.key_reset = Key{(u32)uni(row[4]), (u32)uni(row[5])};
     o.next_master = Key{0u, 0u};
     const int ag = l - 32;
-    o.acts = (ag >= 0) & (ag < na) ? row[6 + (ag < 0 ? 0 : ag)] : 0;
+    o.acts = ((ag >= 0) & (ag < na)) ? row[6 + (ag < 0 ? 0 : ag)] : 0;
     o.shuffle_bits = l < A ? (u32)row[6 + na + (l < A ? l : 0)] : 0u;
     return o;
 }
@@ -2631,8 +2683,9 @@ template <int S> DEV void write_debug(const Book<S>& B, i32* dst) {
 #define MAX_AGENT_ROWS 128
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
-template <int S, int NFIX, bool RC>
-// RC: cancel_mode 2/3 (the random cancel fallback of the engine).
+template <int S, int NFIX, bool RC, bool RA = false>
+// RC: cancel_mode 2/3 (the random cancel fallback of the engine).  RA: the agent rows live in the
+// trade log (lds_map).
 // master: Speed_test rollout mode — the env's step key is split(mk, n_env + 1)[e + 1],
 // actions are sampled here (hftlob_sample_actions) and written to actions_io if it is not
 // NULL; mk becomes split(mk)[0].  Otherwise keys / actions_io are the inputs.  (mk is a
@@ -2655,13 +2708,14 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const int M = c.n_msgs, D = c.n_data_msg, A = c.n_action_msgs, C = c.n_cancel_msgs;
     i32* rec = state + (size_t)e * c.rec_words;
     // LDS: [agent rows (C+A)*8][action extras n_agents*6, 16B-padded][book]
-    i32* rows = lds;
-    i32* axs = rows + (C + A) * 8;
     Book<S> B;
     B.c = lobcfg(c.lob);
     if (NFIX > 0) { B.c.nO = NFIX; B.c.nT = NFIX; }
     const int R = B.c.nO;
-    book_bind(B, axs + ((c.n_agents * 6 + 3) & ~3));
+    const LdsMap LM = lds_map(c, B.c.nO, B.c.nT, RA);
+    i32* rows = lds + LM.rows;
+    i32* axs = lds + LM.axs;
+    book_bind(B, lds + LM.book);
     SideRows<S> fa, fb;  // issue the book's HBM loads first; they land while the keys are derived
     if (!resident) {
         fetch_side(fa, rec + c.off_asks, B.vs);
@@ -2848,7 +2902,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 
     STAMP(t_agents);
     // ---- (B)+(D) stream the combined messages through the book, 64 per chunk
-    trades_fill(B.tr, B.vt, -1);
+    if (!RA) trades_fill(B.tr, B.vt, -1);
     B.ntr = 0;
     const int AR = C + A;
     bool abort_any = false;
@@ -2876,6 +2930,10 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             const i32* g = msg_data + (size_t)(dstart + row + 64 - AR) * 8;
             nx = reinterpret_cast<const int4*>(g)[0];
             ny = reinterpret_cast<const int4*>(g)[1];
+        }
+        if (RA && (base == 0)) {  // the step's trade log starts all -1: reset once chunk 0's agent rows,
+            lds_order();          // which live in it, are read (a wave's LDS operations run in order)
+            trades_fill(B.tr, B.vt, -1);
         }
         decode_msgs(B.c, x, y);
         i32 rpa = 0, rqa = 0, rpb = 0, rqb = 0;
@@ -2938,6 +2996,12 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     wv.dt = dt;
     i32* info = info_out ? info_out + (size_t)e * c.info_words : nullptr;
     {
+        // the step's trade log as the rewards read it, loaded once for every agent
+        TradeView<S> TV;
+        {
+            const i32 ovr0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            trade_view(B, TV, false, -1, ovr0);
+        }
         int ag = 0;
         i32* st = rec + c.off_agents;
         for (int t = 0; t < c.n_types; ++t) {
@@ -2964,7 +3028,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 #ifdef HFTLOB_KO_REWARD  // timing knockout builds only (wrong results)
                     memset(&R, 0, sizeof R);
 #else
-                    mm_reward(c, tc, B, X, s, tid, excl_any, R);
+                    mm_reward(c, tc, B, X, s, tid, excl_any, TV, R);
 #endif
                     STAMP_ACC(acc_mmr, tr0);
                     const float tot = bitf(s[3]) + R.PnL;
@@ -2985,7 +3049,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 #ifdef HFTLOB_KO_REWARD
                     memset(&R, 0, sizeof R);
 #else
-                    exe_reward(c, tc, B, X, s, tid, R);
+                    exe_reward(c, tc, B, X, s, tid, TV, R);
 #endif
                     STAMP_ACC(acc_exr, tr0);
                     s[2] = wadd(s[2], R.agentQuant);
@@ -3070,7 +3134,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 // split over key_n envs (split(master, key_n + 1)[key_e0 + e + 1]); a full-batch
 // launch has key_e0 = 0, key_n = n_env.  Block 0 writes the carried master key
 // split(master, key_n + 1)[0] to master_out.
-template <int S, int NFIX, bool RC>
+template <int S, int NFIX, bool RC, bool RA = false>
 __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, int key_e0, int key_n,
                                                  const u32* __restrict__ keys, const u32* __restrict__ master,
                                                  u32* __restrict__ master_out, i32* __restrict__ actions_io,
@@ -3082,7 +3146,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
     Key mk{0u, 0u};
     if (master) mk = Key{master[0], master[1]};
     u32 fl = 0;
-    env_step_dev<S, NFIX, RC>(c, key_n, key_e0 + e, e, keys, master != nullptr, mk, actions_io, msg_data, init_states,
+    env_step_dev<S, NFIX, RC, RA>(c, key_n, key_e0 + e, e, keys, master != nullptr, mk, actions_io, msg_data, init_states,
                               state, out.obs, out.rewards, out.done_all, out.dones, out.info, out.obs_raw, out.msgs,
                               out.debug, lds, false, false, fl);
     if (master && (e == 0) && (lane_id() == 0)) { master_out[0] = mk.a; master_out[1] = mk.b; }
@@ -3139,7 +3203,7 @@ DEV void balance_prio(unsigned long long* row, u32 slot, unsigned long long r0, 
     else if (q == 2) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 }
-template <int S, int NFIX, bool RC>
+template <int S, int NFIX, bool RC, bool RA = false>
 __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_env, int key_e0, int key_n, int n_steps,
                                                     int per_step, const u32* __restrict__ master,
                                                     u32* __restrict__ master_out, i32* __restrict__ actions_io,
@@ -3173,8 +3237,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
     // the key batches (step_keys_batch) live after the book in LDS
     const bool kbat = kb_ok(c);
     const int kbw = kb_words(c);
-    i32* kbuf = lds + (c.n_cancel_msgs + c.n_action_msgs) * 8 + ((c.n_agents * 6 + 3) & ~3) +
-                12 * (NFIX > 0 ? NFIX : c.lob.n_orders) + 8 * (NFIX > 0 ? NFIX : c.lob.n_trades) + 256;
+    i32* kbuf = lds + lds_map(c, NFIX > 0 ? NFIX : c.lob.n_orders, NFIX > 0 ? NFIX : c.lob.n_trades, RA).kb;
 #pragma unroll 1
     for (int t = 0; t < n_steps; ++t) {
         const size_t o = per_step ? (size_t)t * n_env : 0;
@@ -3188,7 +3251,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         STAMP(kb0);
         if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
         STAMP(kb1);
-        const bool reset = env_step_dev<S, NFIX, RC>(
+        const bool reset = env_step_dev<S, NFIX, RC, RA>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
             out.dones + o * cc.n_agents, out.info ? out.info + o * cc.info_words : nullptr,
@@ -3199,7 +3262,11 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
         STAMP(bp0);
 #ifndef HFTLOB_NO_BALANCE
-        if (t + 1 < n_steps) balance_prio(bal_row, bal_slot, bal_r0, t + 1, n_steps - t - 1);
+#ifndef HFTLOB_BALANCE_EVERY
+#define HFTLOB_BALANCE_EVERY 1
+#endif
+        if ((t + 1 < n_steps) && ((t % HFTLOB_BALANCE_EVERY) == 0))
+            balance_prio(bal_row, bal_slot, bal_r0, t + 1, n_steps - t - 1);
 #endif
 #ifdef HFTLOB_STAMPS
         // rollout-only phases beside env_step_dev's stamps: the step-key batch (every KB_STEPS-th
@@ -3270,8 +3337,8 @@ __global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__
                          hftlob_step_out
 #define HFTLOB_ROLL_ARGS hftlob_env_cfg, int, int, int, int, int, const u32*, u32*, i32*, const i32*, const i32*, i32*, \
                          hftlob_step_out
-#define HFTLOB_STEP(P, SS, NF, RC) P template __global__ void k_env_step<SS, NF, RC>(HFTLOB_STEP_ARGS);
-#define HFTLOB_ROLL(P, SS, NF, RC) P template __global__ void k_env_rollout<SS, NF, RC>(HFTLOB_ROLL_ARGS);
+#define HFTLOB_STEP(P, SS, NF, RC) P template __global__ void k_env_step<SS, NF, RC, false>(HFTLOB_STEP_ARGS);
+#define HFTLOB_ROLL(P, SS, NF, RC) P template __global__ void k_env_rollout<SS, NF, RC, false>(HFTLOB_ROLL_ARGS);
 #define HFTLOB_PART1(P) HFTLOB_ROLL(P, 2, 100, false)
 #define HFTLOB_PART2(P) HFTLOB_STEP(P, 2, 100, false)
 #define HFTLOB_PART3(P) HFTLOB_ROLL(P, 1, 0, false) HFTLOB_STEP(P, 1, 0, false)
@@ -3279,6 +3346,8 @@ __global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__
 #define HFTLOB_PART5(P) HFTLOB_ROLL(P, 4, 0, false) HFTLOB_STEP(P, 4, 0, false)
 #define HFTLOB_PART6(P) HFTLOB_ROLL(P, 1, 0, true) HFTLOB_STEP(P, 1, 0, true) HFTLOB_ROLL(P, 2, 0, true)
 #define HFTLOB_PART7(P) HFTLOB_STEP(P, 2, 0, true) HFTLOB_ROLL(P, 4, 0, true) HFTLOB_STEP(P, 4, 0, true)
+#define HFTLOB_PART8(P) P template __global__ void k_env_rollout<2, 100, false, true>(HFTLOB_ROLL_ARGS); \
+                        P template __global__ void k_env_step<2, 100, false, true>(HFTLOB_STEP_ARGS);
 #define HFTLOB_NONE
 #if defined(HFTLOB_INST)
 #if HFTLOB_INST == 1
@@ -3295,11 +3364,13 @@ HFTLOB_PART5(HFTLOB_NONE)
 HFTLOB_PART6(HFTLOB_NONE)
 #elif HFTLOB_INST == 7
 HFTLOB_PART7(HFTLOB_NONE)
+#elif HFTLOB_INST == 8
+HFTLOB_PART8(HFTLOB_NONE)
 #endif
 #else  // the main translation unit
 #if !defined(HFTLOB_SINGLE_TU)
 HFTLOB_PART1(extern) HFTLOB_PART2(extern) HFTLOB_PART3(extern) HFTLOB_PART4(extern)
-HFTLOB_PART5(extern) HFTLOB_PART6(extern) HFTLOB_PART7(extern)
+HFTLOB_PART5(extern) HFTLOB_PART6(extern) HFTLOB_PART7(extern) HFTLOB_PART8(extern)
 #endif
 
 // ================================================================ C ABI
@@ -3450,10 +3521,19 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
 #ifndef HFTLOB_LDS_FLOOR
 #define HFTLOB_LDS_FLOOR 0
 #endif
+// the 100/100 kernel (launched for these configs; the others take the general-size kernels)
+static bool nfix_kernel(const hftlob_env_cfg* cfg) {
+    return cfg->lob.cancel_mode < 2 && cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0 &&
+           !has_fixed_prices(cfg);
+}
+// the rows-in-trades layout where it raises the envs a CU holds: the 100/100 kernel, rows that
+// fit (rows_in_trades) and a per-env LDS above the 16 waves' share of a CU (160 KB / 16)
+static bool use_rows_alias(const hftlob_env_cfg* cfg) {
+    return nfix_kernel(cfg) && rows_in_trades(*cfg, cfg->lob.n_trades) &&
+           4 * lds_map(*cfg, cfg->lob.n_orders, cfg->lob.n_trades, false).words > 160 * 1024 / 16;
+}
 static size_t env_shm(const hftlob_env_cfg* cfg) {
-    const size_t b = 4 * ((size_t)(cfg->n_cancel_msgs + cfg->n_action_msgs) * 8 + ((cfg->n_agents * 6 + 3) & ~3) +
-                          12 * cfg->lob.n_orders + 8 * cfg->lob.n_trades + 64 * 4 +
-                          (kb_ok(*cfg) ? KB_STEPS * kb_words(*cfg) : 0));
+    const size_t b = 4 * (size_t)lds_map(*cfg, cfg->lob.n_orders, cfg->lob.n_trades, use_rows_alias(cfg)).words;
     return b < (size_t)HFTLOB_LDS_FLOOR ? (size_t)HFTLOB_LDS_FLOOR : b;
 }
 
@@ -3472,9 +3552,11 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int
         if (S == 1) LAUNCH_STEP(1, 0, true);
         else if (S == 2) LAUNCH_STEP(2, 0, true);
         else LAUNCH_STEP(4, 0, true);
-    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0 &&
-               !has_fixed_prices(cfg))  // the 100/100 kernel has no MultiDiscrete / fixed_prices path
-        LAUNCH_STEP(2, 100, false);
+    } else if (nfix_kernel(cfg)) {  // the 100/100 kernel has no MultiDiscrete / fixed_prices path
+        if (use_rows_alias(cfg)) hipLaunchKernelGGL((k_env_step<2, 100, false, true>), g, b, shm, st, kc, n_env, key_e0,
+                                                    key_n, keys, key_in, key_out, actions, msg_data, init_states, state, *out);
+        else LAUNCH_STEP(2, 100, false);
+    }
     else if (S == 1) LAUNCH_STEP(1, 0, false);
     else if (S == 2) LAUNCH_STEP(2, 0, false);
     else LAUNCH_STEP(4, 0, false);
@@ -3498,8 +3580,12 @@ static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, 
         if (S == 1) LAUNCH_ROLL(1, 0, true);
         else if (S == 2) LAUNCH_ROLL(2, 0, true);
         else LAUNCH_ROLL(4, 0, true);
-    } else if (cfg->lob.n_orders == 100 && cfg->lob.n_trades == 100 && cfg->ep_type == 0 && !has_fixed_prices(cfg))
-        LAUNCH_ROLL(2, 100, false);
+    } else if (nfix_kernel(cfg)) {
+        if (use_rows_alias(cfg)) hipLaunchKernelGGL((k_env_rollout<2, 100, false, true>), g, b, shm, st, kc, n_env,
+                                                    key_e0, key_n, n_steps, per_step, key_in, key_out, actions, msg_data,
+                                                    init_states, state, *out);
+        else LAUNCH_ROLL(2, 100, false);
+    }
     else if (S == 1) LAUNCH_ROLL(1, 0, false);
     else if (S == 2) LAUNCH_ROLL(2, 0, false);
     else LAUNCH_ROLL(4, 0, false);

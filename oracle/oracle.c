@@ -202,7 +202,8 @@ long long oracle_stats[32];
 /* per-message class trace (tools/msg_runs.py): 0 doNothing, 1 add behind / at the best, 2 add
  * improving the best, 3 crossing add, 4 add into a full side, 5 cancel of quantity 0, 6 cancel
  * found by id, 7 cancel found by the init-id fallback, 8 cancel of no row into an empty last
- * slot, 9 cancel of no row into an occupied last slot */
+ * slot, 9 cancel of no row into an occupied last slot, 10 as 8 but an init-id row at the price
+ * holds less than the cancel's quantity */
 signed char oracle_trace[1 << 24];
 long long oracle_trace_n;
 #else
@@ -477,6 +478,11 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
                 if (r[0] == m.price && r[2] <= c->init_id && r[2] >= lo && r[1] >= m.qty) { idx = i; break; }
             }
             cls = idx >= 0 ? 7 : (sd[(nO - 1) * 6] == -1 ? 8 : 9);
+            if (cls == 8) /* an init-id row at the price, but with a smaller quantity (10) */
+                for (int i = 0; i < nO; ++i) {
+                    const i32* r = sd + i * 6;
+                    if (r[0] == m.price && r[2] <= c->init_id && r[2] >= lo) { cls = 10; break; }
+                }
         }
     } else {
         const i32* own = index == 1 ? bids : asks;

@@ -61,6 +61,29 @@ for _ in range(30):
     L.hftlob_env_rollout_sampled(*args)
     bare.append(time.perf_counter() - t0)
 torch.cuda.synchronize()
+# where the Python wrapper's time goes: to the C call (pre-launch), the C call, after it
+orig = env._abi
+marks = {}
+
+
+def timed_abi(fn, *a):
+    marks["enter"] = time.perf_counter()
+    orig(fn, *a)
+    marks["exit"] = time.perf_counter()
+
+
+env._abi = timed_abi
+pre, post, ccall = [], [], []
+for _ in range(30):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    env.rollout_sampled(k0, k1, state, params, T, n_slices=0)
+    t1 = time.perf_counter()
+    pre.append(marks["enter"] - t0)
+    ccall.append(marks["exit"] - marks["enter"])
+    post.append(t1 - marks["exit"])
+env._abi = orig
+torch.cuda.synchronize()
 # a synchronised empty round trip (event record + synchronize): the completion latency floor
 rt = []
 for _ in range(30):
@@ -72,4 +95,5 @@ for _ in range(30):
 med = lambda x: float(np.median(x)) * 1e6  # noqa: E731
 print(f"steps {T}: wall {med(wall):.1f} us, events {med(ev):.1f} us, host call {med(host):.1f} us, "
       f"empty sync round trip {med(rt):.1f} us, wall - events {med(wall) - med(ev):.1f} us, "
-      f"bare ctypes launch call {med(bare):.1f} us")
+      f"bare ctypes launch call {med(bare):.1f} us; wrapper: before _abi {med(pre):.1f} us, _abi (device / "
+      f"stream lookup + C call) {med(ccall):.1f} us, after it (results) {med(post):.1f} us")

@@ -11,7 +11,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "jaxmarl-hft_amd")]
 import numpy as np  # noqa: E402
 
 CLS = ["doNothing", "add behind/at best", "add improving best", "crossing add", "add into full side",
-       "cancel qty 0", "cancel by id", "cancel by init id", "cancel no row, last empty", "cancel no row, last used"]
+       "cancel qty 0", "cancel by id", "cancel by init id", "cancel no row, last empty", "cancel no row, last used",
+       "no row, last empty, init row < qty"]
 
 
 def main():
@@ -46,7 +47,7 @@ def main():
     seq = tr.reshape(-1, M)  # per env-step (the oracle runs env by env, step by step)
     runs = []
     for row in seq:
-        live = row[~np.isin(row, (0, 5, 8))]   # the kernel skips these already
+        live = row[~np.isin(row, (0, 5, 8, 10))]   # the kernel skips these (10: only with an exact init test)
         r = 0
         for v in live:
             if v == 1:
@@ -58,7 +59,11 @@ def main():
         if r:
             runs.append(r)
     runs = np.array(runs)
-    live_n = np.sum(~np.isin(tr, (0, 5, 8)))
+    live_n = np.sum(~np.isin(tr, (0, 5, 8, 10)))
+    st = tr.reshape(-1, M)
+    T_ = st.shape[0] // E
+    by_step = np.array([np.mean(st.reshape(E, T_, M)[:, t] == 10) for t in range(T_)]) * M
+    print("class-10 messages per env-step by episode step:", np.round(by_step[:20], 2).tolist())
     print(f"processed messages per step: {live_n / len(seq):.1f}; simple adds per step {np.sum(tr == 1) / len(seq):.1f}")
     print(f"runs of simple adds: {len(runs) / len(seq):.1f} per step, mean length {runs.mean():.2f}; "
           f"length histogram {np.bincount(runs)[1:12].tolist()}")

@@ -18,7 +18,7 @@ if [ "$G" = 0 ]; then
 else
   KER=k_env_step; STATS_ARGS=""; PMC_ARGS="--warmup 4 --steps 32"; SPL=1; SSPL=1
 fi
-echo "{\"kernel\": \"$KER\", \"slices\": $G, \"steps_per_launch\": $SPL, \"stats_steps_per_launch\": $SSPL}" > $O/shape.json
+echo "{\"kernel\": \"$KER\", \"slices\": $G, \"steps_per_launch\": $SPL, \"stats_steps_per_launch\": $SSPL, \"commit\": \"${PROF_COMMIT:-}\"}" > $O/shape.json
 [ -n "$SKIP_TESTS" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || exit 8
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 9
 timeout -k 10 600 python bench.py --slices $G > $O/bench.json 2> $O/bench.err || exit 1
@@ -37,4 +37,14 @@ timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY --output-format csv -d $O/lds -o run -- $B $PMC_ARGS > $O/lds.log 2>&1 || exit 6
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python bench.py --mode step --no-cpu-baseline > $O/bench_stepmode.json 2> $O/bench_stepmode.err || exit 7
+# the driver's command itself (20 steps, CPU baseline included) and the other configs' bench lines
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || exit 10
+timeout -k 10 300 python bench.py --envs 512 --no-cpu-baseline > $O/bench_c2_512.json 2> $O/bench_c2.err || exit 11
+timeout -k 10 300 python bench.py --config 3_player_fq_fqc_dir --envs 1024 --no-cpu-baseline > $O/bench_c5_1024.json 2> $O/bench_c5.err || exit 12
+# phase stamps of the rollout kernel at the driver's launch length (needs ab/stamps.so: make -C jaxmarl-hft_amd/csrc stamps)
+if [ -f ab/stamps.so ]; then
+  ST_STEPS=20 timeout -k 10 300 python tools/diag_stamps_rollout.py > $O/stamps_rollout20.txt 2> $O/stamps.err || exit 13
+  ST_STEPS=128 timeout -k 10 300 python tools/diag_stamps_rollout.py > $O/stamps_rollout128.txt 2>> $O/stamps.err || exit 13
+fi
+timeout -k 10 200 python tools/diag_host.py > $O/diag_host.txt 2> $O/diag_host.err || exit 14
 python $GRAFT_REPO_ROOT/tools/summarize_profiles.py $O > $O/summary.txt 2>&1

@@ -110,7 +110,8 @@ prof = dict(kstat or {})
 if kstat20:
     prof["rocprof_20_step_launch"] = kstat20
 prof.update({"kernel": KERNEL, "slices": shape.get("slices", G), "envs_per_launch": E // G,
-             "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d))})
+             "launches_in_flight": G, "source": os.path.basename(os.path.normpath(d)),
+             "commit": shape.get("commit") or os.environ.get("PROF_COMMIT")})
 if "INSTS_SALU" in per_wave20:
     prof["salu_per_env_step_by_launch_steps"] = {str(SPL): per_wave.get("INSTS_SALU"), "20": per_wave20["INSTS_SALU"]}
 if "INSTS_SALU" in per_wave:
