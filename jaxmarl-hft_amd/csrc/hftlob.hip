@@ -2824,7 +2824,19 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 }
                 ActX x{0, 0, 0, 0, 0, 0};
                 STAMP(ta0);
+#if defined(HFTLOB_KO_ACT) || defined(HFTLOB_KO_CNL)  // timing knockout builds only (wrong results)
+                for (int k = 0; k < tc.n_msgs; ++k) {
+#ifndef HFTLOB_KO_ACT
+                    if (k < tc.n_action_msgs) continue;
+#endif
+#ifndef HFTLOB_KO_CNL
+                    if (k >= tc.n_action_msgs) continue;
+#endif
+                    put_row(rows, k < tc.n_action_msgs ? arow + k : crow + k - tc.n_action_msgs, 0, 0, 0, 0, 0, 0, 0, 0);
+                }
+#endif
                 if (tc.kind == HFTLOB_AGENT_MM) {
+#ifndef HFTLOB_KO_ACT
                     if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
                         mm_directional(c, tc, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
                     else if (tc.action_space == HFTLOB_MM_ACT_FIXED_QUANTS)
@@ -2832,22 +2844,29 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     else
                         mm_other_actions(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, ld_t0, rows,
                                          arow, x);
+#endif
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
                     const int sz = tc.n_msgs / 4;
+#ifndef HFTLOB_KO_CNL
                     cancel_rows(B.b, R, B.vs, tid, sz, 1, wt0, wt1, rows, crow);
                     cancel_rows(B.a, R, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
+#endif
                     STAMP_ACC(acc_cnl, ta1);
                 } else {
+#ifndef HFTLOB_KO_ACT
                     if (NFIX == 0 && tc.action_space == HFTLOB_EXE_ACT_FIXED_PRICES)
                         exe_fixed_prices(c, tc, rec, s4, tid, av, wt0, wt1, rows, arow);
                     else
                         exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, max_steps, rows, arow);
+#endif
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
+#ifndef HFTLOB_KO_CNL
                     const i32 sell = s4[3];
                     cancel_rows(sell ? B.a : B.b, R, B.vs, tid, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
                                 crow);
+#endif
                     STAMP_ACC(acc_cnl, ta1);
                 }
                 STAMP(ta2);
