@@ -9,6 +9,13 @@
   a compile run (here: W warm-up steps), then the timed run of K steps from the same
   state0 and master_key.
 
+Before the timed run the GPU is brought to the clock it holds under sustained load (untimed,
+--settle-ms, default 25 ms of back-to-back rollout steps, then state0 and master_key restored):
+the chip raises its clock over the first milliseconds of load, and a 20-step timed launch
+(1.3 ms) after a 5-step warm-up ran at ≈3 % lower clock than the same launch after a longer one
+(profiles/r04_warmup_sensitivity.txt).  An RL training loop steps its envs back to back, so the
+settled clock is the one it sees.  The JSON line reports what ran (`clock_settle`).
+
 The K timed steps are one MARLEnv.rollout_sampled call (hftlob_env_rollout_sampled,
 Speed_test's whole scan): split + sample + step fused.  By default (MARLEnv.default_slices)
 that is ONE persistent k_env_rollout launch while the whole batch is resident on the GPU (the
@@ -55,6 +62,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="GPUs = ranks (one process per GPU)")
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--settle-ms", type=float, default=25.0,
+                    help="untimed back-to-back rollout steps (at least this much wall time) after the warm-up, "
+                         "so the timed run starts at the clock the GPU holds under load; 0 = off")
     ap.add_argument("--envs", type=int, default=NUM_ENVS, help="envs per GPU")
     ap.add_argument("--n-msgs", type=int, default=400_000, help="synthetic day length (messages)")
     ap.add_argument("--mid", type=int, default=2_000_000)
@@ -368,6 +378,15 @@ def main(argv=None):
         nstep[0] = 0
 
     run(args.warmup)                          # Speed_test's compile run
+    # clock settle (untimed): 64-step calls until --settle-ms of wall time has passed, then back to
+    # state0 / master_key; the timed run below is unchanged by it (same state, same K steps)
+    torch.cuda.synchronize()
+    settle_steps, ts0 = 0, time.perf_counter()
+    while args.settle_ms > 0 and (time.perf_counter() - ts0) * 1e3 < args.settle_ms and settle_steps < 64 * 256:
+        run(64)
+        settle_steps += 64
+        torch.cuda.synchronize()
+    settle_ms = (time.perf_counter() - ts0) * 1e3
     restart()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
@@ -468,6 +487,8 @@ def main(argv=None):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "clock_settle": {"steps": settle_steps, "ms": round(settle_ms, 1), "untimed": True,
+                         "then": "state0 and master_key restored; the timed run starts from them"},
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",

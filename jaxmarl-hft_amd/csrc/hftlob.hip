@@ -89,6 +89,24 @@ DEV float ffloordiv(float x, float y) {
     return roundf(div);
 }
 
+// jnp.floor_divide(x, float(tick_size)) for float32 x: with y = tick_size an integer below 2^24
+// and |x| < 2^24, ffloordiv returns floor(x / y) exactly (fmod_exact is exact, x - fmod(x, y) is
+// y * trunc(x / y), an integer below 2^24, so the division is exact and the floor adjustment is
+// the real floor; x = -0 gives +0).  Here, for a = |x|: k = floor(a * rcp(y)) is floor(a / y) or
+// off by one (a / y < 2^19, rcp within 4 ulp), and the remainder r = a - k y is exact (a multiple of ulp(a), below
+// y and no larger than a once corrected), so one correction step gives floor(a / y) and r; then
+// floor(x / y) = -(floor(a / y) + (r != 0)) for x < 0.  Outside those bounds (and NaN / inf) it
+// takes ffloordiv.  tools/ffloordiv_check.c checks it bit for bit against the jnp formula.
+DEV float tick_ffloordiv(const hftlob_env_cfg& c, float x) {
+    const float y = (float)c.tick_size, a = fabsf(x);
+    const float q = a * __builtin_amdgcn_rcpf(y);
+    if (!((a < 16777216.0f) & (q < 524288.0f) & (c.tick_size < (1 << 24)))) return ffloordiv(x, y);
+    float k = floorf(q), r = fmaf(-k, y, a);
+    if (r < 0.0f) { k -= 1.0f; r += y; }
+    else if (r >= y) { k += 1.0f; r -= y; }
+    return (x < 0.0f ? -(k + (r != 0.0f ? 1.0f : 0.0f)) : k) + 0.0f;
+}
+
 // DPP all-reduce across the wave; result is wave-uniform (SGPR).
 // quad_perm[1,0,3,2], quad_perm[2,3,0,1], row_half_mirror, row_mirror,
 // row_bcast:15 (rows 1,3), row_bcast:31 (rows 2,3) -> lane 63 holds the total.
@@ -1713,7 +1731,7 @@ DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int 
 // `scratch`: 16 words of LDS.
 template <int n>
 DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
-    __syncthreads();
+    lds_order();  // (one-wave workgroups: the rows written above are read back in order, no barrier)
     const int l = lane_id();
     const bool is_a = l < n, is_c = (l >= 8) & (l < 8 + n);
     const int row = is_a ? arow + l : (is_c ? crow + l - 8 : arow);
@@ -1744,7 +1762,7 @@ DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
     } else if (is_a | is_c) {
         lds_rows[row * 8 + 2] = nq;
     }
-    __syncthreads();
+    lds_order();
 }
 
 // MM _getActionMsgs_fixedQuant — mm_env.py:970-1118
@@ -1783,7 +1801,7 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
     i32 ba, bb;
     const bool empty = masked_best(c, B, tid, last_ba, last_bb, ba, bb);
     const float hsp = fmaxf(i2f(wsub(ba, bb)) / 2.0f, (float)tick / 2.0f);
-    const float hs = (ffloordiv(hsp, (float)tick) + 1.0f) * (float)tick;
+    const float hs = (tick_ffloordiv(c, hsp) + 1.0f) * (float)tick;
     float bo, ao;
     i32 bq, aq;
     if (!tc.sell_buy_all_option) {
@@ -1809,8 +1827,8 @@ DEV void mm_fixed_quant(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc
     if (empty) { bq = 0; aq = 0; }
     const float bpf = i2f(bb) - bo * hs;
     const float apf = i2f(ba) + ao * hs;
-    const i32 bp = f2i(ffloordiv(fmaxf(bpf, 0.0f), (float)tick) * (float)tick);
-    const i32 ap = f2i(ffloordiv(fmaxf(i2f(wadd(bp, tick)), apf), (float)tick) * (float)tick);
+    const i32 bp = f2i(tick_ffloordiv(c, fmaxf(bpf, 0.0f)) * (float)tick);
+    const i32 ap = f2i(tick_ffloordiv(c, fmaxf(i2f(wadd(bp, tick)), apf)) * (float)tick);
     i32 typ0 = 1, typ1 = 1, sd0 = 1, sd1 = -1, qq0 = bq, qq1 = aq, pp0 = bp, pp1 = ap;
     const i32 inv = st[2];
     const i32 lq0 = f2i(tc.auto_liquidate_alpha * i2f(imax_(wsub(0, inv), 0)));
@@ -1874,8 +1892,8 @@ DEV void mm_other_actions(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& 
             float bf = res - spread / 2.0f, af = res + spread / 2.0f;
             bf = fminf(fmaxf(bf, 0.0f), (float)c.lob.maxint);
             af = fminf(fmaxf(af, 0.0f), (float)c.lob.maxint);
-            bp = f2i_sat(ffloordiv(bf, (float)tick) * (float)tick);
-            ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
+            bp = f2i_sat(tick_ffloordiv(c, bf) * (float)tick);
+            ap = f2i_sat(tick_ffloordiv(c, af) * (float)tick);
             const i32 q = tick_floordiv(c, mid), rm = wsub(mid, wmul(q, tick));
             bp = imin_(bp, wmul(wsub(q, rm == 0 ? 1 : 0), tick));  // round_down: strictly below mid
             ap = imax_(ap, wmul(wadd(q, 1), tick));                // round_up: strictly above mid
@@ -1893,8 +1911,8 @@ DEV void mm_other_actions(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& 
             const float skt = sk == 0 ? -tc.skew_multiplier : (sk == 1 ? 0.0f : tc.skew_multiplier);
             const float smid = mid + skt * (tc.multiplier_type ? nsp : (float)tick);
             const float hs = ffloordiv(nsp, 2.0f);
-            bp = f2i_sat(ffloordiv(smid - hs, (float)tick) * (float)tick);
-            ap = f2i_sat(ffloordiv(smid + hs, (float)tick) * (float)tick);
+            bp = f2i_sat(tick_ffloordiv(c, smid - hs) * (float)tick);
+            ap = f2i_sat(tick_ffloordiv(c, smid + hs) * (float)tick);
             bq = fq; aq = fq;
         } else {  // simple :1123-1246
             const float bo = ai == 1 ? -2000.0f : 0.0f, ao = ai == 2 ? -2000.0f : 0.0f;
@@ -1910,8 +1928,8 @@ DEV void mm_other_actions(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& 
             // entry 3 (simple_nothing_action) is all zeros; with 3 entries `ai` clamps to 2
             const float to = (float)wmul(tc.n_ticks_offset, tick);
             const float bf = i2f(bb) - bo * to, af = i2f(ba) + ao * to;
-            bp = f2i_sat(ffloordiv(fmaxf(bf, 0.0f), (float)tick) * (float)tick);
-            ap = f2i_sat(ffloordiv(af, (float)tick) * (float)tick);
+            bp = f2i_sat(tick_ffloordiv(c, fmaxf(bf, 0.0f)) * (float)tick);
+            ap = f2i_sat(tick_ffloordiv(c, af) * (float)tick);
         }
     }
     const i32 ta = wadd(wt0, tc.time_delay_obs_act), tb = wadd(wt1, tc.time_delay_obs_act);
@@ -1945,7 +1963,7 @@ DEV void exe_fqc(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const
     i32 pl[4];
     if (sell) {
         pl[0] = bb;
-        pl[1] = f2i(ceilf(ffloordiv(i2f(wadd(bb, ba)) / 2.0f, (float)tick)) * (float)tick);
+        pl[1] = f2i(ceilf(tick_ffloordiv(c, i2f(wadd(bb, ba)) / 2.0f)) * (float)tick);
         pl[2] = ba;
         pl[3] = wadd(ba, wmul(tick, tc.n_ticks_in_book));
     } else {
@@ -2324,11 +2342,11 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
             refp = sell ? wmul(tick_floordiv(c, wsub(X.last_bb, pen)), tick)
                         : wmul(tick_floordiv(c, wadd(X.last_ba, pen)), tick);
         else if (tc.reference_price == HFTLOB_PRICE_FAR_TOUCH)  // int32 price - Python float: f32
-            refp = sell ? f2i(ffloordiv(i2f(X.last_bb) - penf, (float)tick) * (float)tick)
-                        : f2i(ffloordiv(i2f(X.last_ba) + penf, (float)tick) * (float)tick);
+            refp = sell ? f2i(tick_ffloordiv(c, i2f(X.last_bb) - penf) * (float)tick)
+                        : f2i(tick_ffloordiv(c, i2f(X.last_ba) + penf) * (float)tick);
         else
-            refp = sell ? f2i(ffloordiv(X.avg_mid - penf, (float)tick) * (float)tick)
-                        : f2i(ffloordiv(X.avg_mid + penf, (float)tick) * (float)tick);
+            refp = sell ? f2i(tick_ffloordiv(c, X.avg_mid - penf) * (float)tick)
+                        : f2i(tick_ffloordiv(c, X.avg_mid + penf) * (float)tick);
         if (quant_left > 0) {
             const i32 ovr[8] = {refp, wmul(side_sign, iabs_(quant_left)), c.artificial_order_id,
                                 c.placeholder_order_id, 0, 0, c.artificial_trader_id, tid};
@@ -2361,7 +2379,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
         dur_sum = rows_fsum(dur, nT);
     }
     float pv;
-    if (oq == 0) pv = ffloordiv(X.avg_mid, (float)tick);
+    if (oq == 0) pv = tick_ffloordiv(c, X.avg_mid);
     else {
         float vw[S];
 #pragma unroll
@@ -2374,7 +2392,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     }
     const i32 dirs = isign(wsub(wmul(sell, 2), 1));
     const float adv = i2f(dirs) * (i2f(qp) - pv * i2f(aq));
-    const float drift = i2f(wmul(dirs, aq)) * (pv - ffloordiv(init_price, (float)tick));
+    const float drift = i2f(wmul(dirs, aq)) * (pv - tick_ffloordiv(c, init_price));
     const float slip = adv + drift;
     const float scf = i2f(X.step), sc1 = i2f(wadd(X.step, 1));
     DivBatch D{lane_id()};  // the per-agent averages, then the rolling means (exec_env.py:1760-1762)
@@ -2835,39 +2853,49 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     put_row(rows, k < tc.n_action_msgs ? arow + k : crow + k - tc.n_action_msgs, 0, 0, 0, 0, 0, 0, 0, 0);
                 }
 #endif
+#ifdef HFTLOB_DUP_AGENT  // timing builds only: the agent's action and cancel rows computed twice
+                i32 z_ = 0;     // (an opaque zero keeps the second pass from being hoisted or merged)
+                asm volatile("s_mov_b32 %0, 0" : "=s"(z_));
+                for (int rep = 0; rep < 2; ++rep) {
+                const i32 tid_r = tid ^ (rep * z_), act_r = act ^ (rep * z_), ba_r = old_last_ba ^ (rep * z_);
+#else
+                {
+                const i32 tid_r = tid, act_r = act, ba_r = old_last_ba;
+#endif
                 if (tc.kind == HFTLOB_AGENT_MM) {
 #ifndef HFTLOB_KO_ACT
                     if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
-                        mm_directional(c, tc, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
+                        mm_directional(c, tc, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, rows, arow, x);
                     else if (tc.action_space == HFTLOB_MM_ACT_FIXED_QUANTS)
-                        mm_fixed_quant(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, rows, arow, x);
+                        mm_fixed_quant(c, tc, B, s4, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, rows, arow, x);
                     else
-                        mm_other_actions(c, tc, B, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, ld_t0, rows,
+                        mm_other_actions(c, tc, B, s4, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, step, ld_t0, rows,
                                          arow, x);
 #endif
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
                     const int sz = tc.n_msgs / 4;
 #ifndef HFTLOB_KO_CNL
-                    cancel_rows(B.b, R, B.vs, tid, sz, 1, wt0, wt1, rows, crow);
-                    cancel_rows(B.a, R, B.vs, tid, sz, -1, wt0, wt1, rows, crow + sz);
+                    cancel_rows(B.b, R, B.vs, tid_r, sz, 1, wt0, wt1, rows, crow);
+                    cancel_rows(B.a, R, B.vs, tid_r, sz, -1, wt0, wt1, rows, crow + sz);
 #endif
                     STAMP_ACC(acc_cnl, ta1);
                 } else {
 #ifndef HFTLOB_KO_ACT
                     if (NFIX == 0 && tc.action_space == HFTLOB_EXE_ACT_FIXED_PRICES)
-                        exe_fixed_prices(c, tc, rec, s4, tid, av, wt0, wt1, rows, arow);
+                        exe_fixed_prices(c, tc, rec, s4, tid_r, av, wt0, wt1, rows, arow);
                     else
-                        exe_fqc(c, tc, s4, tid, act, wt0, wt1, old_last_ba, old_last_bb, step, max_steps, rows, arow);
+                        exe_fqc(c, tc, s4, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, step, max_steps, rows, arow);
 #endif
                     STAMP_ACC(acc_act, ta0);
                     STAMP(ta1);
 #ifndef HFTLOB_KO_CNL
                     const i32 sell = s4[3];
-                    cancel_rows(sell ? B.a : B.b, R, B.vs, tid, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
+                    cancel_rows(sell ? B.a : B.b, R, B.vs, tid_r, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
                                 crow);
 #endif
                     STAMP_ACC(acc_cnl, ta1);
+                }
                 }
                 STAMP(ta2);
                 {
@@ -2890,7 +2918,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             }
         }
     }
-    __syncthreads();
+    lds_order();
     STAMP(t_rows);
     // order ids (counter - j) and the action-row permutation (lane j = action row j)
     {
@@ -2911,12 +2939,12 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             }
             dest = rank;
         }
-        __syncthreads();
+        lds_order();
         if (act_lane) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) rows[(C + dest) * 8 + k] = f[k];
         }
-        __syncthreads();
+        lds_order();
     }
 
     STAMP(t_agents);
