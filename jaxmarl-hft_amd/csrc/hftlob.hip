@@ -2853,18 +2853,21 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     put_row(rows, k < tc.n_action_msgs ? arow + k : crow + k - tc.n_action_msgs, 0, 0, 0, 0, 0, 0, 0, 0);
                 }
 #endif
-#ifdef HFTLOB_DUP_AGENT  // timing builds only: the agent's action and cancel rows computed twice
+#ifdef HFTLOB_DUP_AGENT  // timing builds only: the agent's action (bit 0) / cancel (bit 1) rows computed twice
                 i32 z_ = 0;     // (an opaque zero keeps the second pass from being hoisted or merged)
                 asm volatile("s_mov_b32 %0, 0" : "=s"(z_));
                 for (int rep = 0; rep < 2; ++rep) {
                 const i32 tid_r = tid ^ (rep * z_), act_r = act ^ (rep * z_), ba_r = old_last_ba ^ (rep * z_);
+                const bool do_act = rep == 0 || (HFTLOB_DUP_AGENT & 1), do_cnl = rep == 0 || (HFTLOB_DUP_AGENT & 2);
 #else
                 {
                 const i32 tid_r = tid, act_r = act, ba_r = old_last_ba;
+                constexpr bool do_act = true, do_cnl = true;
 #endif
                 if (tc.kind == HFTLOB_AGENT_MM) {
 #ifndef HFTLOB_KO_ACT
-                    if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
+                    if (!do_act) {
+                    } else if (tc.action_space == HFTLOB_MM_ACT_DIRECTIONAL)
                         mm_directional(c, tc, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, rows, arow, x);
                     else if (tc.action_space == HFTLOB_MM_ACT_FIXED_QUANTS)
                         mm_fixed_quant(c, tc, B, s4, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, rows, arow, x);
@@ -2876,13 +2879,16 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     STAMP(ta1);
                     const int sz = tc.n_msgs / 4;
 #ifndef HFTLOB_KO_CNL
-                    cancel_rows(B.b, R, B.vs, tid_r, sz, 1, wt0, wt1, rows, crow);
-                    cancel_rows(B.a, R, B.vs, tid_r, sz, -1, wt0, wt1, rows, crow + sz);
+                    if (do_cnl) {
+                        cancel_rows(B.b, R, B.vs, tid_r, sz, 1, wt0, wt1, rows, crow);
+                        cancel_rows(B.a, R, B.vs, tid_r, sz, -1, wt0, wt1, rows, crow + sz);
+                    }
 #endif
                     STAMP_ACC(acc_cnl, ta1);
                 } else {
 #ifndef HFTLOB_KO_ACT
-                    if (NFIX == 0 && tc.action_space == HFTLOB_EXE_ACT_FIXED_PRICES)
+                    if (!do_act) {
+                    } else if (NFIX == 0 && tc.action_space == HFTLOB_EXE_ACT_FIXED_PRICES)
                         exe_fixed_prices(c, tc, rec, s4, tid_r, av, wt0, wt1, rows, arow);
                     else
                         exe_fqc(c, tc, s4, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, step, max_steps, rows, arow);
@@ -2891,8 +2897,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     STAMP(ta1);
 #ifndef HFTLOB_KO_CNL
                     const i32 sell = s4[3];
-                    cancel_rows(sell ? B.a : B.b, R, B.vs, tid_r, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1, rows,
-                                crow);
+                    if (do_cnl)
+                        cancel_rows(sell ? B.a : B.b, R, B.vs, tid_r, tc.n_msgs / 2, wsub(1, wmul(sell, 2)), wt0, wt1,
+                                    rows, crow);
 #endif
                     STAMP_ACC(acc_cnl, ta1);
                 }
