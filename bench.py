@@ -378,13 +378,14 @@ def main(argv=None):
         nstep[0] = 0
 
     run(args.warmup)                          # Speed_test's compile run
-    # clock settle (untimed): 64-step calls until --settle-ms of wall time has passed, then back to
-    # state0 / master_key; the timed run below is unchanged by it (same state, same K steps)
+    # clock settle (untimed): calls of the timed run's length (T steps, so every launch a profiler
+    # sees is the timed shape) until --settle-ms of wall time has passed, then back to state0 /
+    # master_key; the timed run below is unchanged by it (same state, same K steps)
     torch.cuda.synchronize()
     settle_steps, ts0 = 0, time.perf_counter()
-    while args.settle_ms > 0 and (time.perf_counter() - ts0) * 1e3 < args.settle_ms and settle_steps < 64 * 256:
-        run(64)
-        settle_steps += 64
+    while args.settle_ms > 0 and (time.perf_counter() - ts0) * 1e3 < args.settle_ms and settle_steps < 16384:
+        run(T)
+        settle_steps += T
         torch.cuda.synchronize()
     settle_ms = (time.perf_counter() - ts0) * 1e3
     restart()
