@@ -38,16 +38,21 @@ static void check(float x, int tick) {
         }
     }
 }
-int main(void) {
+int main(int argc, char** argv) {
+    /* argv[1] == "quick" (tests/test_tick_division.py): the grid at +-4000 multiples and every
+     * 65521st bit pattern */
+    const int quick = argc > 1 && argv[1][0] == 'q';
+    const long long mmax = quick ? 4000 : 40000;
+    const uint64_t bstep = quick ? 65521 : 1021;
     const int ticks[] = {1, 2, 3, 7, 10, 25, 100, 128, 1000, 12345, 65537, 1 << 20, (1 << 24) - 1, 1 << 24};
     for (unsigned t = 0; t < sizeof ticks / sizeof ticks[0]; ++t) {
         const int tick = ticks[t];
-        for (long long m = -40000; m <= 40000; ++m)  /* around multiples of the tick */
+        for (long long m = -mmax; m <= mmax; ++m)  /* around multiples of the tick */
             for (int d = -8; d <= 8; ++d) {
                 const double xv = (double)m * tick + d * 0.25;
                 if (fabs(xv) < 16777216.0) check((float)xv, tick);
             }
-        for (uint64_t u = 0; u < 0x80000000ull; u += 1021) {  /* float bit patterns, both signs */
+        for (uint64_t u = 0; u < 0x80000000ull; u += bstep) {  /* float bit patterns, both signs */
             uint32_t v = (uint32_t)u;
             float x;
             memcpy(&x, &v, 4);
