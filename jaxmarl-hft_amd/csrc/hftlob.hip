@@ -183,11 +183,21 @@ DEV float self(bool c, float a, float b) {  // (uniform floats live in VGPRs: th
 
 // Diagnostic build only (-DHFTLOB_STAMPS): per-phase shader-clock stamps of
 // k_env_step, written to the info buffer in place of the info fields.
+// STAMP marks the step's top phases, SUBSTAMP / STAMP_ACC the sub-phases; each read of the clock
+// waits for the wave's outstanding scalar and LDS operations, so the sub-phase probes slow the
+// phases they sit in: -DHFTLOB_STAMPS_COARSE keeps the top phases only (words 5..14 then 0).
 #ifdef HFTLOB_STAMPS
 #define STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#ifdef HFTLOB_STAMPS_COARSE
+#define SUBSTAMP(var) const unsigned long long var = 0
+#define STAMP_ACC(acc, since)
+#else
+#define SUBSTAMP(var) STAMP(var)
 #define STAMP_ACC(acc, since) acc += __builtin_amdgcn_s_memtime() - since
+#endif
 #else
 #define STAMP(var)
+#define SUBSTAMP(var)
 #define STAMP_ACC(acc, since)
 #endif
 
@@ -2753,7 +2763,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         B.nmsg = M;
         B.part = c.prng_partitionable;
     }
-    STAMP(t_keys);
+    SUBSTAMP(t_keys);
     // loaded / world scalars (wave-uniform)
     const i32* Lr = rec + c.off_loaded;
     const i32* Wr = rec + c.off_world;
@@ -2795,7 +2805,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs) | F_STALE_A | F_STALE_B;
         B.fl |= fast_bit(B.fl);
     }
-    STAMP(t_load);
+    SUBSTAMP(t_load);
 
     // ---- (C) agent messages -> LDS rows [cancels C][actions A]
 #ifdef HFTLOB_STAMPS
@@ -2841,7 +2851,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     for (int k = 0; k < 4; ++k) s4[k] = agw_pre ? rdl(agw, b + k) : st[k];
                 }
                 ActX x{0, 0, 0, 0, 0, 0};
-                STAMP(ta0);
+                SUBSTAMP(ta0);
 #if defined(HFTLOB_KO_ACT) || defined(HFTLOB_KO_CNL)  // timing knockout builds only (wrong results)
                 for (int k = 0; k < tc.n_msgs; ++k) {
 #ifndef HFTLOB_KO_ACT
@@ -2876,7 +2886,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                                          arow, x);
 #endif
                     STAMP_ACC(acc_act, ta0);
-                    STAMP(ta1);
+                    SUBSTAMP(ta1);
                     const int sz = tc.n_msgs / 4;
 #ifndef HFTLOB_KO_CNL
                     if (do_cnl) {
@@ -2894,7 +2904,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                         exe_fqc(c, tc, s4, tid_r, act_r, wt0, wt1, ba_r, old_last_bb, step, max_steps, rows, arow);
 #endif
                     STAMP_ACC(acc_act, ta0);
-                    STAMP(ta1);
+                    SUBSTAMP(ta1);
 #ifndef HFTLOB_KO_CNL
                     const i32 sell = s4[3];
                     if (do_cnl)
@@ -2904,7 +2914,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     STAMP_ACC(acc_cnl, ta1);
                 }
                 }
-                STAMP(ta2);
+                SUBSTAMP(ta2);
                 {
                     const i32 xv[6] = {x.bid_price, x.ask_price, x.bid_dist, x.ask_dist, x.bid_quant, x.ask_quant};
                     i32 v = 0;
@@ -2926,7 +2936,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         }
     }
     lds_order();
-    STAMP(t_rows);
+    SUBSTAMP(t_rows);
     // order ids (counter - j) and the action-row permutation (lane j = action row j)
     {
         i32 f[8];
@@ -3076,7 +3086,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 ax1.bid_price = uni(axs[ag * 6 + 0]); ax1.ask_price = uni(axs[ag * 6 + 1]);
                 ax1.bid_dist = uni(axs[ag * 6 + 2]); ax1.ask_dist = uni(axs[ag * 6 + 3]);
                 ax1.bid_quant = uni(axs[ag * 6 + 4]); ax1.ask_quant = uni(axs[ag * 6 + 5]);
-                STAMP(tr0);
+                SUBSTAMP(tr0);
                 if (tc.kind == HFTLOB_AGENT_MM) {
                     MMRew R;
 #ifdef HFTLOB_KO_REWARD  // timing knockout builds only (wrong results)
@@ -3128,7 +3138,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     for (int k = 0; k < HFTLOB_INFO_AGENT_WORDS; ++k) if (l == k) v = iw[k];
                     if (l < HFTLOB_INFO_AGENT_WORDS) info[HFTLOB_INFO_WORLD_WORDS + ag * HFTLOB_INFO_AGENT_WORDS + l] = v;
                 }
-                STAMP(to0);
+                SUBSTAMP(to0);
                 if (!all) {  // stepped state + obs survive only when the episode continues
                     i32 v = 0;
                     for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
@@ -3163,8 +3173,13 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
         info[0] = (i32)(t_agents - t_start); info[1] = (i32)(t_book - t_agents);
         info[2] = (i32)(t_rewards - t_book); info[3] = (i32)(t_end - t_rewards); info[4] = (i32)all;
+#ifndef HFTLOB_STAMPS_COARSE
         info[5] = (i32)(t_keys - t_start); info[6] = (i32)(t_load - t_keys); info[7] = (i32)(t_rows - t_load);
         info[8] = (i32)(t_agents - t_rows);
+#else
+        info[5] = info[6] = info[7] = info[8] = 0;
+        (void)t_keys; (void)t_load; (void)t_rows;
+#endif
         info[9] = (i32)acc_act; info[10] = (i32)acc_cnl; info[11] = (i32)acc_flt;
         info[12] = (i32)acc_mmr; info[13] = (i32)acc_exr; info[14] = (i32)acc_obs;
         info[15] = (i32)(__builtin_amdgcn_s_memrealtime() - rt_start);

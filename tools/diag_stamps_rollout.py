@@ -8,6 +8,9 @@ writes its phase stamps into words 0..15 of each step's info row and whose rollo
 step-key batch (word 16, every 4th step) and the issue-priority update (word 17).  Prints the
 median / mean cycles and the share of each phase per env-step.  The stamp build's absolute time
 is not the product's (the stamps cost a few hundred cycles per step); read its shares.
+HFTLOB_STAMPS_LIB=ab/stamps_coarse.so (the same build without the sub-phase probes, which wait for
+the wave's outstanding LDS and scalar operations inside the phases they time) gives the top
+phases' shares with less perturbation.
 """
 import os
 import sys
@@ -50,7 +53,8 @@ names = ["step-key batch (every 4th step)", "setup+agent msgs+shuffle", "112-msg
          "store+info", "issue priority"]
 for i, n in enumerate(names):
     print(f"  {n:32s} median {np.median(top[:, i]):9.0f}  mean {top[:, i].mean():9.0f}  share {top[:, i].sum() / tot.sum():.3f}")
-for i, n in zip(range(5, 15), ["  setup: step keys (LDS row)", "  setup: relink / load book", "  setup: agent rows",
+print(f"stamp build: {os.path.basename(os.environ['HFTLOB_LIB'])}" + (" (top phases only)" if not r[:, 5:15].any() else ""))
+for i, n in zip(range(5, 15) if r[:, 5:15].any() else [], ["  setup: step keys (LDS row)", "  setup: relink / load book", "  setup: agent rows",
                               "  setup: ids + shuffle", "    agents: action msgs", "    agents: cancel rows",
                               "    agents: filter", "  rewards: MM reward", "  rewards: EXE reward",
                               "  rewards: state + obs writes"]):
