@@ -1708,35 +1708,27 @@ DEV void put_row(i32* lds_rows, int row, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4,
     if (l < 8) lds_rows[row * 8 + l] = v;
 }
 
-// getCancelMsgs — JaxOrderBookArrays.py:827-853, lane-parallel: the k-th book row (in row order)
-// holding the agent's id writes cancel row row0 + k from its own lane, lanes n..size-1 the
-// zero-filled rows of the jnp.where fill (index -1 = the appended all-zero row)
+// getCancelMsgs — JaxOrderBookArrays.py:827-853
 template <int S>
 DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int size, i32 side, i32 t, i32 tns,
                      i32* lds_rows, int row0) {
-    const int l = lane_id();
     int n = 0;
-    i32 tid[S], q[S], o[S];
+    i32 tid[S], q[S], o[S];  // one LDS round trip; hit rows are read from registers
     const i32 (&p)[S] = s.pc;
     ldcol(s.t, R, FTID, tid);
     ldcol(s.t, R, FQ, q);
     ldcol(s.t, R, FOID, o);
 #pragma unroll
     for (int r = 0; r < S; ++r) {
-        const lmask bm = V.m[r] & bal(tid[r] == agent);
-        const int k = n + (int)lanes_below(bm);
-        if (((bm >> l) & 1ull) && (k < size)) {
-            int4* d = reinterpret_cast<int4*>(lds_rows + (row0 + k) * 8);
-            d[0] = make_int4(2, side, q[r], p[r]);
-            d[1] = make_int4(o[r], agent, t, tns);
+        lmask bm = V.m[r] & bal(tid[r] == agent);
+        while (bm && n < size) {
+            const int ln = (int)__builtin_ctzll(bm);
+            bm &= bm - 1;
+            put_row(lds_rows, row0 + n, 2, side, rdl(q[r], ln), rdl(p[r], ln), rdl(o[r], ln), agent, t, tns);
+            ++n;
         }
-        n += __builtin_popcountll(bm);
     }
-    if ((l >= n) & (l < size)) {
-        int4* d = reinterpret_cast<int4*>(lds_rows + (row0 + l) * 8);
-        d[0] = make_int4(2, side, 0, 0);
-        d[1] = make_int4(0, 0, t, tns);
-    }
+    for (; n < size; ++n) put_row(lds_rows, row0 + n, 2, side, 0, 0, 0, 0, t, tns);
 }
 
 // _filter_messages — mm_env.py:520-582 == exec_env.py:413-475, lane-parallel:
