@@ -3089,7 +3089,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 SUBSTAMP(tr0);
                 if (tc.kind == HFTLOB_AGENT_MM) {
                     MMRew R;
-#ifdef HFTLOB_KO_REWARD  // timing knockout builds only (wrong results)
+#if defined(HFTLOB_KO_REWARD) || defined(HFTLOB_KO_MM_REWARD)  // timing knockout builds only (wrong results)
                     memset(&R, 0, sizeof R);
 #else
                     mm_reward(c, tc, B, X, s, tid, excl_any, TV, R);
@@ -3110,7 +3110,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     iw[23] = fbit(R.inventoryValue);
                 } else {
                     EXRew R;
-#ifdef HFTLOB_KO_REWARD
+#if defined(HFTLOB_KO_REWARD) || defined(HFTLOB_KO_EXE_REWARD)
                     memset(&R, 0, sizeof R);
 #else
                     exe_reward(c, tc, B, X, s, tid, TV, R);
