@@ -93,10 +93,11 @@ DEV float ffloordiv(float x, float y) {
 // and |x| < 2^24, ffloordiv returns floor(x / y) exactly (fmod_exact is exact, x - fmod(x, y) is
 // y * trunc(x / y), an integer below 2^24, so the division is exact and the floor adjustment is
 // the real floor; x = -0 gives +0).  Here, for a = |x|: k = floor(a * rcp(y)) is floor(a / y) or
-// off by one (a / y < 2^19, rcp within 4 ulp), and the remainder r = a - k y is exact (a multiple of ulp(a), below
-// y and no larger than a once corrected), so one correction step gives floor(a / y) and r; then
-// floor(x / y) = -(floor(a / y) + (r != 0)) for x < 0.  Outside those bounds (and NaN / inf) it
-// takes ffloordiv.  tools/ffloordiv_check.c checks it bit for bit against the jnp formula.
+// off by one (a / y < 2^19, rcp within 4 ulp), and the remainder r = a - k y is exact (a multiple
+// of ulp(a), below y and no larger than a once corrected), so one correction step gives
+// floor(a / y) and r; then floor(x / y) = -(floor(a / y) + (r != 0)) for x < 0.  Outside those
+// bounds (and NaN / inf) it takes ffloordiv.  tools/ffloordiv_check.c checks it bit for bit
+// against the jnp formula.
 DEV float tick_ffloordiv(const hftlob_env_cfg& c, float x) {
     const float y = (float)c.tick_size, a = fabsf(x);
     const float q = a * __builtin_amdgcn_rcpf(y);
