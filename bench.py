@@ -377,7 +377,28 @@ def main(argv=None):
         kbuf[0].copy_(master0)
         nstep[0] = 0
 
+    stream = torch.cuda.current_stream(dev)
+
+    def timed():  # the K timed steps from (state0, master0): barrier + sync on both sides, max over ranks
+        restart()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        D.barrier(R)
+        torch.cuda.synchronize()
+        D.barrier(R)
+        t0 = time.perf_counter()
+        ev0.record(stream)                    # on the launch stream (slice 0 runs on it; the others join it)
+        run(args.steps)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        D.barrier(R)
+        el = time.perf_counter() - t0
+        return D.max_over_ranks(R, el, device=red_dev), ev0.elapsed_time(ev1) / args.steps
+
     run(args.warmup)                          # Speed_test's compile run
+    # the same K steps timed right after the warm-up, as Speed_test times them (reported beside
+    # `value` as `unsettled`: the GPU has not reached its loaded clock yet)
+    uns_elapsed, uns_kern_ms = timed() if args.settle_ms > 0 else (None, None)
     # clock settle (untimed): calls of the timed run's length (T steps, so every launch a profiler
     # sees is the timed shape) until --settle-ms of wall time has passed, then back to state0 /
     # master_key; the timed run below is unchanged by it (same state, same K steps)
@@ -388,22 +409,7 @@ def main(argv=None):
         settle_steps += T
         torch.cuda.synchronize()
     settle_ms = (time.perf_counter() - ts0) * 1e3
-    restart()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    D.barrier(R)
-    torch.cuda.synchronize()
-    D.barrier(R)
-    t0 = time.perf_counter()
-    ev0.record(stream)                        # on the launch stream (slice 0 runs on it; the others join it)
-    run(args.steps)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    D.barrier(R)
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps     # HIP-event time of the timed region per batched step
-    elapsed = D.max_over_ranks(R, elapsed, device=red_dev)
+    elapsed, kern_ms = timed()                # kern_ms: HIP-event time of the timed region per batched step
     if args.dump_state:  # this rank's end state and carried key (tests/test_gpu_bench_ranks.py)
         os.makedirs(args.dump_state, exist_ok=True)
         np.savez(os.path.join(args.dump_state, f"rank{rank}.npz"), state=state.buf.cpu().numpy(),
@@ -488,8 +494,16 @@ def main(argv=None):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        # untimed steps the GPU ran before the timed K: the W warm-up, the unsettled timing run and the settle
+        "warmup_effective": args.warmup + (args.steps if uns_elapsed is not None else 0) + settle_steps,
         "clock_settle": {"steps": settle_steps, "ms": round(settle_ms, 1), "untimed": True,
                          "then": "state0 and master_key restored; the timed run starts from them"},
+        "unsettled": ({"value": round(world * E * args.steps / uns_elapsed, 1),
+                       "ms_per_step": round(uns_elapsed / args.steps * 1e3, 4),
+                       "kernel_ms": round(uns_kern_ms, 5),
+                       "what": (f"the same {args.steps} steps from state0 timed right after the {args.warmup} "
+                                "warm-up steps, before the clock settle (Speed_test's order; --settle-ms 0 "
+                                "makes this the value)")} if uns_elapsed is not None else None),
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",

@@ -337,6 +337,23 @@ int hftlob_rollout_prepare(int n_slices, void* stream);
  * once); it replaces nothing in the reference, whose XLA compiler sizes its own buffers. */
 int hftlob_env_lds_bytes(const hftlob_env_cfg* cfg /*[host]*/);
 
+/* Which kernel instantiation hftlob_env_step / hftlob_env_rollout_sampled launch for this
+ * config, and the launch-derived constants they pass it (host-only, no device call).  Tests
+ * use it to assert which code path a parity case ran; it replaces nothing in the reference.
+ *   slot_sets     register sets per lane (1, 2 or 4: n_orders / n_trades up to 64 / 128 / 256)
+ *   nfix          100: the 100/100-slot specialisation; 0: the general-size kernel
+ *   random_cancel 1: the cancel_mode 2/3 (get_random_id_match) instantiation
+ *   rows_alias    1: the agents' message rows live inside the trade log (the layout that
+ *                 raises the envs a CU holds, e.g. Speed_test's [5, 5] agents)
+ *   lds_bytes     dynamic LDS per env workgroup (hftlob_env_lds_bytes)
+ *   tick_magic    the multiplier of the exact floor division by tick_size the kernels use,
+ *                 ceil(2^(31+l) / tick_size), l = ceil(log2 tick_size) */
+typedef struct hftlob_launch_info {
+    int32_t slot_sets, nfix, random_cancel, rows_alias, lds_bytes;
+    uint32_t tick_magic;
+} hftlob_launch_info;
+int hftlob_env_launch_info(const hftlob_env_cfg* cfg /*[host]*/, hftlob_launch_info* out /*[host]*/);
+
 /* Speed_test action sampling (Speed_test.py:166-177, gymnax Discrete.sample):
  * for env e with step key k_e,
  * sub = split(k_e, n_types); per type t, agent i:

@@ -3753,6 +3753,21 @@ int hftlob_env_lds_bytes(const hftlob_env_cfg* cfg) {
     return rc ? rc : (int)env_shm(cfg);
 }
 
+int hftlob_env_launch_info(const hftlob_env_cfg* cfg, hftlob_launch_info* out) {
+    const int rc = check_env(cfg);
+    if (rc) return rc;
+    if (!out) return fail(HFTLOB_ENULL, "null out");
+    // the selection env_step_launch / env_rollout_launch make
+    const bool rcm = cfg->lob.cancel_mode >= 2, nf = !rcm && nfix_kernel(cfg);
+    out->slot_sets = nf ? 2 : slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
+    out->nfix = nf ? 100 : 0;
+    out->random_cancel = rcm ? 1 : 0;
+    out->rows_alias = nf && use_rows_alias(cfg) ? 1 : 0;
+    out->lds_bytes = (int)env_shm(cfg);
+    out->tick_magic = kernel_cfg(cfg).tick_magic;
+    return HFTLOB_OK;
+}
+
 int hftlob_rollout_prepare(int n_slices, void* stream) {
     if (n_slices < 0 || n_slices > ROLLOUT_MAX_SLICES) return fail(HFTLOB_EINVAL, "n_slices must be 0..4");
     if (n_slices <= 1) return HFTLOB_OK;  // no library stream needed

@@ -11,11 +11,17 @@ import os
 
 from .layout import EnvCfg, LobCfg, StepOut
 
+
+class LaunchInfo(C.Structure):
+    """hftlob_launch_info (include/hftlob.h): the kernel instantiation a config launches."""
+    _fields_ = [("slot_sets", C.c_int32), ("nfix", C.c_int32), ("random_cancel", C.c_int32),
+                ("rows_alias", C.c_int32), ("lds_bytes", C.c_int32), ("tick_magic", C.c_uint32)]
+
 LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
 ABI_VERSION = 7
 EXPORTS = ("hftlob_version", "hftlob_last_error", "hftlob_book_process", "hftlob_env_reset",
            "hftlob_env_step", "hftlob_env_step_sampled", "hftlob_env_rollout_sampled", "hftlob_rollout_prepare",
-           "hftlob_env_lds_bytes",
+           "hftlob_env_lds_bytes", "hftlob_env_launch_info",
            "hftlob_sample_actions", "hftlob_split_keys")
 
 _lib = None
@@ -52,6 +58,8 @@ def lib() -> C.CDLL:
     L.hftlob_rollout_prepare.restype = i32
     L.hftlob_env_lds_bytes.argtypes = [C.POINTER(EnvCfg)]
     L.hftlob_env_lds_bytes.restype = i32
+    L.hftlob_env_launch_info.argtypes = [C.POINTER(EnvCfg), C.POINTER(LaunchInfo)]
+    L.hftlob_env_launch_info.restype = i32
     L.hftlob_sample_actions.argtypes = [C.POINTER(EnvCfg), i32, vp, vp, vp]
     L.hftlob_sample_actions.restype = i32
     L.hftlob_split_keys.argtypes = [i32, i32, i32, vp, vp, vp]

@@ -205,6 +205,9 @@ class MARLEnv:
         self.persistent_outputs = persistent_outputs
         self._out = None
         self._init_states = self._precompute_init_states()
+        # the device every launch goes to: the one this env's tensors were allocated on, fixed here
+        # (not whichever device is current at the first launch)
+        self._dev_idx = self._init_states.device.index
 
     # BaseLOBEnv._init_states (base_env.py:298-333) on the GPU engine
     def _precompute_init_states(self) -> torch.Tensor:
@@ -394,8 +397,7 @@ class MARLEnv:
     def _dev_index(self) -> int:
         i = self.__dict__.get("_dev_idx")
         if i is None:
-            i = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            self.__dict__["_dev_idx"] = i
+            raise RuntimeError(f"MARLEnv on {self._init_states.device}: the hftlob kernels need a HIP device")
         return i
 
     # ------------------------------------------------------------------ API
@@ -462,6 +464,14 @@ class MARLEnv:
         if n <= 0:
             _lib.check(n)
         return n
+
+    def launch_info(self) -> dict:
+        """The kernel instantiation step / rollout_sampled launch for this config
+        (hftlob_env_launch_info): slot_sets, nfix (100 = the 100/100 specialisation),
+        random_cancel, rows_alias (agent rows inside the trade log), lds_bytes, tick_magic."""
+        info = _lib.LaunchInfo()
+        _lib.check(_lib.lib().hftlob_env_launch_info(C.byref(self.cfg_c), C.byref(info)))
+        return {k: int(getattr(info, k)) for k, _ in info._fields_}
 
     def _tuned_device(self) -> bool:
         if not torch.cuda.is_available():

@@ -461,7 +461,8 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
     long long before = oracle_stats[20];
     i32 ba0[2], bb0[2], ba1[2], bb1[2];
     best_quotes(c, asks, bids, ba0, bb0);
-#endif
+    /* the message's class for the stats trace (tools/msg_mix.py): only the stats build pays these
+       O(nOrders) scans; the checker and the CPU baseline skip them */
     int cls = -1;
     if (index == 4) cls = 0;
     else if (index >= 2) {
@@ -490,6 +491,7 @@ static void process_msg(const hftlob_lob_cfg* c, const i32* d, i32* asks, i32* b
         for (int i = 0; i < nO; ++i) full &= own[i * 6] >= 0;
         cls = full ? 4 : 1;
     }
+#endif
     switch (index) {
         case 0: ask_lim(c, m, asks, bids, trades); break;
         case 1: bid_lim(c, m, asks, bids, trades); break;

@@ -172,5 +172,37 @@ def test_env_lds_bytes(L, name, agents, part, kb):
              and ar <= c.lob.n_trades and rest + 4 * ar * 8 > 160 * 1024 // 16)
     assert alias == (agents == [5, 5])
     assert L.hftlob_env_lds_bytes(C.byref(c)) == rest + (0 if alias else 4 * ar * 8)
+    info = _lib.LaunchInfo()
+    assert L.hftlob_env_launch_info(C.byref(c), C.byref(info)) == 0
+    assert (info.slot_sets, info.nfix, info.random_cancel, info.rows_alias) == (2, 100, 0, int(alias))
+    assert info.lds_bytes == L.hftlob_env_lds_bytes(C.byref(c))
     c.ep_type = 2
     assert L.hftlob_env_lds_bytes(C.byref(c)) == -1   # an invalid cfg: its error code
+    assert L.hftlob_env_launch_info(C.byref(c), C.byref(info)) == -1
+
+
+def tick_magic(d: int) -> int:
+    """ceil(2^(31+l) / d), l = ceil(log2 d): the multiplier of tick_floordiv (tools/magic_check.c)"""
+    l = (d - 1).bit_length() if d > 1 else 0
+    return -(-(1 << (31 + l)) // d)
+
+
+@pytest.mark.parametrize("tick", [1, 2, 3, 7, 25, 100, 128, 1000, 12345, 2 ** 24 + 1, 2 ** 31 - 1])
+def test_launch_info_tick_magic(L, tick):
+    """the library derives tick_magic from tick_size for every launch (a caller's value is ignored);
+    the multiplier is < 2^32 and makes (n * m) >> (31 + l) == n // d on sampled int32 numerators"""
+    import dataclasses
+    import numpy as np
+    cfg = builtin_config("2_player_fq_fqc")
+    cfg = dataclasses.replace(cfg, world_config=dataclasses.replace(cfg.world_config, tick_size=tick))
+    c, _ = pack_env_cfg(cfg, 4, 1000, True)
+    c.tick_magic = 12345  # ignored
+    info = _lib.LaunchInfo()
+    assert L.hftlob_env_launch_info(C.byref(c), C.byref(info)) == 0
+    m = tick_magic(tick)
+    assert info.tick_magic == m < 2 ** 32
+    l = (tick - 1).bit_length() if tick > 1 else 0
+    n = np.concatenate([np.arange(0, 5000), np.random.default_rng(tick).integers(0, 2 ** 31, 20000),
+                        2 ** 31 - 1 - np.arange(5000), tick * np.arange(1, 3000) - 1, tick * np.arange(1, 3000)])
+    n = n[(n >= 0) & (n < 2 ** 31)].astype(object)
+    assert all((x * m) >> (31 + l) == x // tick for x in n)

@@ -115,6 +115,42 @@ def test_rank_shard_at_real_size(name, E, part):
     assert (state.world_state.step_counter.cpu().numpy() < T).all()
 
 
+def test_c4_shards_compose_at_real_size():
+    """BASELINE.json C4 at its real size on one GPU: NUM_ENVS = 32768 of 2_player_fq_fqc sharded over
+    8 ranks (ippo_rnn_JAXMARL_pmap.py:292-332).  Each of the 8 shards of 4096 envs runs, one after
+    the other, as its rank would (bench.py --gpus 8: reset keys split(PRNGKey(0), 32769)[1 + 4096 r :
+    1 + 4096 (r + 1)], one persistent launch, key_e0 = 4096 r, key_n = 32768, partitionable
+    threefry), 66 steps across every env's episode end; the 8 end states concatenated, and every
+    shard's carried master key, equal the oracle's single 32768-env rollout.  The 8-GPU run then
+    only adds timing."""
+    N, E, T = 8, 4096, 66
+    cfg = builtin_config("2_player_fq_fqc")
+    day = _metric_day(2_000_000)
+    env = MARLEnv(None, cfg, data=day, return_info=False, persistent_outputs=True)
+    params = env.default_params
+    init = env._init_states.cpu().numpy()
+    all_keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device="cuda"), N * E + 1)[0]
+    o_keys = O.split_keys(np.zeros((1, 2), np.uint32), N * E + 1)[0]
+    assert (all_keys.cpu().numpy().view(np.uint32) == o_keys).all()
+    assert env.default_slices(E) == 0
+    ends, masters, s0 = [], [], []
+    for r in range(N):
+        _, s = env.reset(all_keys[1 + r * E:1 + (r + 1) * E].contiguous(), params)
+        s0.append(s.buf.cpu().numpy())
+        ko = torch.empty(2, dtype=torch.int32, device="cuda")
+        env.rollout_sampled(all_keys[0].clone(), ko, s, params, T, key_e0=r * E, key_n=N * E)
+        torch.cuda.synchronize()
+        ends.append(s.buf.cpu().numpy())
+        masters.append(ko.cpu().numpy().view(np.uint32).copy())
+        del s
+    o_end, o_master = O.rollout_sampled(env.cfg_c, o_keys[0], day.msgs, init, np.concatenate(s0), T)
+    del s0
+    for r in range(N):
+        _compare_state(env, o_end[r * E:(r + 1) * E], ends[r], f"rank {r} of 8 after {T} steps")
+        assert (masters[r] == o_master).all(), f"rank {r}: carried master key"
+        assert (ends[r][:, env.layout.off_loaded + 5] < T).all(), f"rank {r}: every env crossed its episode end"
+
+
 def test_default_launch_shape():
     """MARLEnv.default_slices: the persistent launch while its waves of workgroups are full (the
     metric: 4096 envs at 16 per CU, and whole multiples of it), 2 env slices when the last wave
