@@ -2127,7 +2127,7 @@ struct MMRew {
 // MM get_reward — mm_env.py:2214-2673
 template <int S>
 DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const Book<S>& B, const StepCtx& X,
-                   const i32* st, i32 tid, bool excl_any, const TradeView<S>& TV, MMRew& R) {
+                   const i32* st, i32 tid, bool excl_any, const TradeView<S>& TV, MMRew& R, bool full = true) {
     const int nT = c.lob.n_trades;
     const float tick = (float)c.tick_size;
     TradeView<S> V = TV;  // the step's trades (the unwind below overrides one row of this agent's copy)
@@ -2211,6 +2211,11 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     }
     const i32 new_inv = wsub(wadd(inv, bq), sq);
     const float rebate_income = rebate_value * tc.rebate_factor;
+    if (!full) {  // the state's terms only (the step's reward values are not emitted)
+        const float PnL = income - outgoing + rebate_income;
+        R.PnL = PnL; R.cash = bitf(st[4]) + PnL; R.end_inventory = new_inv;
+        return;
+    }
     float ref_buy, ref_sell, ref;
     i32 rbi = 0, rsi = 0, refi = 0;
     if (ri == HFTLOB_PRICE_MID_AVG) { ref_buy = ref_sell = ref = X.avg_mid; }
@@ -2330,7 +2335,7 @@ struct EXRew {
 // EXE get_reward — exec_env.py:1511-1762
 template <int S>
 DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, const Book<S>& B, const StepCtx& X,
-                    const i32* st, i32 tid, const TradeView<S>& TV, EXRew& R) {
+                    const i32* st, i32 tid, const TradeView<S>& TV, EXRew& R, bool full = true) {
     const int nT = c.lob.n_trades;
     const i32 tick = c.tick_size;
     TradeView<S> V = TV;  // the step's trades (the doom trade below overrides one row of this agent's copy)
@@ -2426,7 +2431,7 @@ DEV void exe_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, co
     R.quant_left = wsub(wsub(task, qe), aq);
     R.reward_info = reward;
     if (tc.reward_function == HFTLOB_EXE_REW_FINISH_FAST) reward = i2f(wsub(0, iabs_(R.quant_left)));
-    if (tc.reward_function == HFTLOB_EXE_REW_SIMPLEST_CASE) {  // :1723-1731: sum (p - init_price) |q|, sign by task
+    if (full && tc.reward_function == HFTLOB_EXE_REW_SIMPLEST_CASE) {  // :1723-1731: sum (p - init_price) |q|, sign by task
         float ps[S];
 #pragma unroll
         for (int r = 0; r < S; ++r) {
@@ -2720,7 +2725,13 @@ template <int S, int NFIX, bool RC, bool RA = false>
 // NULL; mk becomes split(mk)[0].  Otherwise keys / actions_io are the inputs.  (mk is a
 // reference, not a pointer: an address-taken local would live in scratch memory.)
 // key_n / ek: the env count of the step-key split and this env's index in it;
-// e: this env's record / output index
+// e: this env's record / output index.
+// emit (wave-uniform): the step's outputs are wanted.  k_env_rollout with per_step = 0 passes
+// false on every step but the last: Speed_test's scan keeps only the state (its jitted body
+// returns `_, state, _, _, _`, so XLA drops the observations and the reward values, which feed no
+// state), and each step's outputs would be overwritten by the next.  Then the observations, the
+// reward values (not the PnL / cash / inventory / execution statistics the agent states carry),
+// the dones and the output stores are skipped; the state is bit-identical either way.
 DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u32* __restrict__ keys, bool master,
                       Key& mk,
                       i32* __restrict__ actions_io, const i32* __restrict__ msg_data,
@@ -2728,7 +2739,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
                       i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
                       i32* __restrict__ debug_out, i32* lds, bool resident, bool keep, u32& fl_carry,
-                      const i32* pre_keys = nullptr) {
+                      const i32* pre_keys = nullptr, bool emit = true) {
     STAMP(t_start);
 #ifdef HFTLOB_STAMPS
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the in-kernel clock
@@ -2775,7 +2786,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const i32 old_last_ba = rec[c.off_best_asks + (M - 1) * 2], old_last_bb = rec[c.off_best_bids + (M - 1) * 2];
     bool excl_any = false;
     for (int t = 0; t < c.n_types; ++t) {
-        if (c.types[t].kind == HFTLOB_AGENT_MM && c.types[t].exclude_extreme_spreads) {
+        if (emit && c.types[t].kind == HFTLOB_AGENT_MM && c.types[t].exclude_extreme_spreads) {
             bool any = false;
             for (int m = l; m < M; m += 64) {
                 const i32 pa = rec[c.off_best_asks + m * 2], pb = rec[c.off_best_bids + m * 2];
@@ -3044,7 +3055,8 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     // ---- (E) rewards, (G) agent states, (K) observations
     WorldView wv;
     wv.best_ask_p = last_p_a; wv.best_bid_p = last_p_b;
-    wv.vol_a = side_volume(B.a, R, B.vs); wv.vol_b = side_volume(B.b, R, B.vs);
+    wv.vol_a = wv.vol_b = 0;
+    if (emit) { wv.vol_a = side_volume(B.a, R, B.vs); wv.vol_b = side_volume(B.b, R, B.vs); }
     if (debug_out) write_debug(B, debug_out + (size_t)e * HFTLOB_DEBUG_WORDS(B.c.nT));  // before store / reset
     // the book is final: store it now (frees its registers for the rewards).  Not when the
     // auto-reset below rewrites the record anyway, nor while the wave's next step (keep,
@@ -3060,7 +3072,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const float dt = i2f(last_t0) + i2f(last_t1) / 1e9f - i2f(wt0) - i2f(wt1) / 1e9f;  // marl_env.py:496
     wv.dt = dt;
     i32* info = info_out ? info_out + (size_t)e * c.info_words : nullptr;
-    {
+    if (emit | !all) {  // (an unemitted episode end: the auto-reset below replaces every agent state)
         // the step's trade log as the rewards read it, loaded once for every agent
         TradeView<S> TV;
         {
@@ -3093,7 +3105,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 #if defined(HFTLOB_KO_REWARD) || defined(HFTLOB_KO_MM_REWARD)  // timing knockout builds only (wrong results)
                     memset(&R, 0, sizeof R);
 #else
-                    mm_reward(c, tc, B, X, s, tid, excl_any, TV, R);
+                    mm_reward(c, tc, B, X, s, tid, excl_any, TV, R, emit);
 #endif
                     STAMP_ACC(acc_mmr, tr0);
                     const float tot = bitf(s[3]) + R.PnL;
@@ -3114,7 +3126,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
 #if defined(HFTLOB_KO_REWARD) || defined(HFTLOB_KO_EXE_REWARD)
                     memset(&R, 0, sizeof R);
 #else
-                    exe_reward(c, tc, B, X, s, tid, TV, R);
+                    exe_reward(c, tc, B, X, s, tid, TV, R, emit);
 #endif
                     STAMP_ACC(acc_exr, tr0);
                     s[2] = wadd(s[2], R.agentQuant);
@@ -3130,7 +3142,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     iw[4] = fbit(R.drift); iw[5] = fbit(R.advantage); iw[6] = R.doom_quant; iw[7] = s[3];
                     iw[8] = fbit(R.reward_info);
                 }
-                if (l == 0) {
+                if (emit & (l == 0)) {
                     rew_out[(size_t)e * c.n_agents + ag] = rew;
                     dones_out[(size_t)e * c.n_agents + ag] = (u8)(d != 0);
                 }
@@ -3145,7 +3157,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                     for (int k = 0; k < 13; ++k) if (l == k) v = s[k];
                     if (l < nw) st[l] = v;
 #ifndef HFTLOB_KO_OBS  // timing knockout builds only (wrong results)
-                    write_obs<false>(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0, ftime);
+                    if (emit)
+                        write_obs<false>(c, tc, wv, s, obs_out + ((size_t)e * c.n_agents + ag) * c.obs_stride, d != 0,
+                                         ftime);
 #endif
                 }
                 if (obs_raw_out)  // the stepped state's raw obs, also on an episode's last step (info)
@@ -3168,7 +3182,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         for (int k = 0; k < HFTLOB_INFO_WORLD_WORDS; ++k) if (l == k) v = wv_[k];
         if (l < HFTLOB_INFO_WORLD_WORDS) info[l] = v;
     }
-    if (l == 0) done_all_out[e] = (u8)all;
+    if (emit & (l == 0)) done_all_out[e] = (u8)all;
 #ifdef HFTLOB_STAMPS
     if (info && l == 0) {
         const unsigned long long t_end = __builtin_amdgcn_s_memtime();
@@ -3187,8 +3201,8 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     }
 #endif
     if (all) {  // auto-reset: MARLEnv.step selects reset(key_reset) for state and obs
-        env_reset_dev<S>(c, key_reset, init_states, rec, obs_out + (size_t)e * c.n_agents * c.obs_stride, B.vs, B.vt,
-                         ftime);
+        env_reset_dev<S>(c, key_reset, init_states, rec, emit ? obs_out + (size_t)e * c.n_agents * c.obs_stride : nullptr,
+                         B.vs, B.vt, ftime);
         return true;
     }
     if (l == 0) {
@@ -3321,14 +3335,17 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         STAMP(kb0);
         if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
         STAMP(kb1);
+        // per_step = 0: only the last step's outputs are written (env_step_dev's emit)
+        const bool emit = (per_step != 0) | (t + 1 == n_steps);
+        const bool ox = emit;  // (the optional outputs: written by the emitted steps only)
         const bool reset = env_step_dev<S, NFIX, RC, RA>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
-            out.dones + o * cc.n_agents, out.info ? out.info + o * cc.info_words : nullptr,
-            out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
-            out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr,
-            out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds, NFIX > 0 && resident,
-            NFIX > 0 && t + 1 < n_steps, fl, kbat ? kbuf + tb * kbw : nullptr);
+            out.dones + o * cc.n_agents, ox && out.info ? out.info + o * cc.info_words : nullptr,
+            ox && out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
+            ox && out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr,
+            ox && out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds,
+            NFIX > 0 && resident, NFIX > 0 && t + 1 < n_steps, fl, kbat ? kbuf + tb * kbw : nullptr, emit);
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
         STAMP(bp0);
 #ifndef HFTLOB_NO_BALANCE
