@@ -669,6 +669,9 @@ struct Book {
     i32 ntr;
     bool part;
     i32* filt;  // LDS: the 2048-bit id / init-price filter of chunk_noops (64 words)
+    // the filter already holds a superset of the book's ids and init-id rows (built at an earlier
+    // chunk of this step, plus every add id since): the next chunk only inserts its own add ids
+    bool filt_ok;
 };
 
 // message handler codes (the reference's dispatch index) and flags, see decode_msgs
@@ -1223,12 +1226,15 @@ template <int S> DEV int side_room(const Book<S>& B, const Side<S>& s) {
     return ldu(s.t, R, FQ, R - 1) == -1 ? n : -1;
 }
 // x, y: the chunk's decoded messages (decode_msgs), lane = message; cnt: messages in the chunk
-template <bool RC, int S> DEV lmask chunk_noops(const Book<S>& B, const int4& x, const int4& y, int cnt) {
+template <bool RC, int S> DEV lmask chunk_noops(Book<S>& B, const int4& x, const int4& y, int cnt) {
     const int l = lane_id();
     const i32 kind = x.x & H_KIND, qty = x.z, price = x.w, oid = y.x;
     const bool in = l < cnt;
     const lmask nop = bal(in & (kind == H_NOP));
-    if ((i32)B.fl >= 0) return nop;  // not FAST
+    if ((i32)B.fl >= 0) {  // not FAST
+        B.filt_ok = false;
+        return nop;
+    }
     const bool cnl = (kind == H_CNL_ASK) | (kind == H_CNL_BID), add = (kind == H_ASK) | (kind == H_BID);
     const i32 lo = wsub(B.c.init_id, wmul(B.c.depth, 2));
     const u32 span = (u32)wsub(B.c.init_id, lo);
@@ -1238,21 +1244,27 @@ template <bool RC, int S> DEV lmask chunk_noops(const Book<S>& B, const int4& x,
     const lmask zero = bal(in & cnl & (qty == 0)) & before;
     if (RC || (u32)wsub(-1, lo) <= span) return nop | zero;  // (-1 ids would be init-id candidates)
     i32* f = B.filt;
-    f[l] = 0;
-    lds_order();
-    const int R = B.c.nO;
+    if (!B.filt_ok) {  // the book's ids and init-id rows' (price, side), as they are now
+        f[l] = 0;
+        lds_order();
+        const int R = B.c.nO;
 #pragma unroll
-    for (int sd = 0; sd < 2; ++sd) {
-        const Side<S>& s = sd ? B.b : B.a;
-        i32 o[S];
-        ldcol(s.t, R, FOID, o);
+        for (int sd = 0; sd < 2; ++sd) {
+            const Side<S>& s = sd ? B.b : B.a;
+            i32 o[S];
+            ldcol(s.t, R, FOID, o);
 #pragma unroll
-        for (int r = 0; r < S; ++r) {
-            filt_set(f, hash_id(o[r]), B.vs.v[r] & (o[r] != -1));
-            filt_set(f, hash_px(s.pc[r], sd == 0), B.vs.v[r] & ((u32)wsub(o[r], lo) <= span));
+            for (int r = 0; r < S; ++r) {
+                filt_set(f, hash_id(o[r]), B.vs.v[r] & (o[r] != -1));
+                filt_set(f, hash_px(s.pc[r], sd == 0), B.vs.v[r] & ((u32)wsub(o[r], lo) <= span));
+            }
         }
     }
+    // the chunk's add ids.  Only adds write rows (their ids go in here), a row's price never changes and
+    // init-id rows come from nowhere else than an add carrying an init id (a brk message), so without a
+    // brk message the filter stays a superset of the book's ids and init rows for the next chunk
     filt_set(f, hash_id(oid), in & add);
+    B.filt_ok = brk == 0ull;
     lds_order();
     const bool ask = kind == H_CNL_ASK;
     const bool hit = (filt_get(f, hash_id(oid)) | filt_get(f, hash_px(price, ask))) != 0u;
@@ -1278,6 +1290,9 @@ DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, 
     const lmask skip = chunk_noops<RC>(B, x, y, cnt) & live;
 #endif
     lmask todo = live & ~skip;
+#ifdef HFTLOB_KO_LOOP  // timing knockout builds only (wrong results): no message reaches the book
+    todo = 0;
+#endif
     refresh_best(B);
     const i32 cpa = B.a.best_p, cqa = B.a.best_q, cpb = B.b.best_p, cqb = B.b.best_q;  // before the chunk
     if (todo) {
@@ -1323,6 +1338,7 @@ template <int S> DEV void book_bind(Book<S>& B, i32* lds) {
     B.tr.t = lds + 12 * B.c.nO;
     B.tr.R = B.c.nT;
     B.filt = lds + 12 * B.c.nO + 8 * B.c.nT + 128;
+    B.filt_ok = false;
     B.a.scr = B.b.scr = B.tr.scr = lds + 12 * B.c.nO + 8 * B.c.nT + 192;
     B.vs.init(B.c.nO);
     B.vt.init(B.c.nT);
@@ -3269,13 +3285,19 @@ DEV unsigned long long* wave_row(u32 hwid, u32 xcc, u32& slot) {
     slot = ((hwid >> 4) & 3u) * 16u + (hwid & 15u);
     return g_wave_eta + (size_t)cu * 64u;
 }
+// The table row is shared only by the waves of one CU, whose L2 (their XCD's) is common: workgroup
+// scope (L1-bypassing loads, write-through stores) keeps the step's load at L2 latency; agent scope
+// (coherent across XCDs) sent it past the L2 (+0.2 to +0.8 %, profiles/r05_ab_filter_prio.txt)
+#ifndef HFTLOB_PRIO_SCOPE
+#define HFTLOB_PRIO_SCOPE __HIP_MEMORY_SCOPE_WORKGROUP
+#endif
 DEV void balance_prio(unsigned long long* row, u32 slot, unsigned long long r0, int done, int left) {
     const int l = lane_id();
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     const float el = (float)(now - r0);
     const unsigned long long eta = now + (unsigned long long)(el * ((float)left / (float)done));
-    if (l == 0) __hip_atomic_store(row + slot, eta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long v = __hip_atomic_load(row + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l == 0) __hip_atomic_store(row + slot, eta, __ATOMIC_RELAXED, HFTLOB_PRIO_SCOPE);
+    unsigned long long v = __hip_atomic_load(row + l, __ATOMIC_RELAXED, HFTLOB_PRIO_SCOPE);
     v = (u32)l == slot ? eta : v;
     v = ((u32)l >> 4) == (slot >> 4) ? v : 0ull;  // the wave's own SIMD (A/B: +2.6 % over the whole CU)
     const lmask live = bal(v > now);
