@@ -2800,9 +2800,11 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const i32 wt0 = Wr[W_T0], wt1 = Wr[W_T1], oidc = Wr[W_OIDC];
     const float wmid = bitf(Wr[W_MID]);
     const i32 old_last_ba = rec[c.off_best_asks + (M - 1) * 2], old_last_bb = rec[c.off_best_bids + (M - 1) * 2];
-    bool excl_any = false;
+    bool excl_any = false, excl_cfg = false;
     for (int t = 0; t < c.n_types; ++t) {
-        if (emit && c.types[t].kind == HFTLOB_AGENT_MM && c.types[t].exclude_extreme_spreads) {
+        const bool ex = c.types[t].kind == HFTLOB_AGENT_MM && c.types[t].exclude_extreme_spreads;
+        excl_cfg |= ex;
+        if (emit && ex) {
             bool any = false;
             for (int m = l; m < M; m += 64) {
                 const i32 pa = rec[c.off_best_asks + m * 2], pb = rec[c.off_best_bids + m * 2];
@@ -2811,6 +2813,11 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             excl_any = ballot(any) != 0ull;
         }
     }
+    // the step's best-quote arrays go to the record when they can be read: always in k_env_step, on a
+    // persistent rollout's last step, and whenever an MM type excludes extreme spreads (its reward
+    // reads the previous step's arrays).  Otherwise the next step reads only their last row (the
+    // old best quotes above), which the step stores alone; the step after that overwrites the rest.
+    const bool store_best = !keep | excl_cfg;
     // the data window (BaseLOBEnv.get_data_messages, base_env.py:339-369); its
     // first chunk is fetched now, ahead of the agent phase
     i32 dstart = wadd(start_index, wmul(D, step));
@@ -3042,9 +3049,11 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         const i32 cap = ffill(pa, prev_a), cbp = ffill(pb, prev_b);
         prev_a = rdl(cap, cnt - 1);
         prev_b = rdl(cbp, cnt - 1);
-        if (row < M) {
+        if ((row < M) & (store_best | (row == M - 1))) {  // (row M - 1: the one the next step reads)
             reinterpret_cast<int2*>(rec + c.off_best_asks)[row] = make_int2(cap, caq);
             reinterpret_cast<int2*>(rec + c.off_best_bids)[row] = make_int2(cbp, cbq);
+        }
+        if (row < M) {
             const float mf = i2f(wadd(cbp, cap)) / 2.0f;
             mid_acc = base == 0 ? mf : mid_acc + mf;
             pa_acc = base == 0 ? i2f(cap) : pa_acc + i2f(cap);
