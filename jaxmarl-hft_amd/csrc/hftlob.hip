@@ -23,6 +23,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <mutex>
+#include <type_traits>
 #include <limits.h>
 
 #include "../../include/hftlob.h"
@@ -2227,116 +2228,117 @@ DEV void mm_reward(const hftlob_env_cfg& c, const hftlob_agent_type_cfg& tc, con
     }
     const i32 new_inv = wsub(wadd(inv, bq), sq);
     const float rebate_income = rebate_value * tc.rebate_factor;
-    if (!full) {  // the state's terms only (the step's reward values are not emitted)
-        const float PnL = income - outgoing + rebate_income;
-        R.PnL = PnL; R.cash = bitf(st[4]) + PnL; R.end_inventory = new_inv;
-        return;
-    }
-    float ref_buy, ref_sell, ref;
-    i32 rbi = 0, rsi = 0, refi = 0;
-    if (ri == HFTLOB_PRICE_MID_AVG) { ref_buy = ref_sell = ref = X.avg_mid; }
-    else if (ref_int) {
-        const bool far = ri == HFTLOB_PRICE_FAR_TOUCH;
-        rbi = sel(far, X.last_ba, X.last_bb);
-        rsi = sel(far, X.last_bb, X.last_ba);
-        refi = new_inv > 0 ? rbi : rsi;
-        ref_buy = i2f(rbi); ref_sell = i2f(rsi); ref = i2f(refi);
-    } else { ref_buy = ref_sell = ref = X.last_mid; }
     const float PnL = income - outgoing + rebate_income;
     const float cash = bitf(st[4]) + PnL;
-    const i32 traded = wadd(bq, sq);
-    const float mid_end = X.last_mid;
-    float old_ref;
-    if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_ba, X.old_last_bb));
-    else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_bb, X.old_last_ba));
-    else old_ref = X.wmid;
-    DivBatch D{lane_id()};
-    D.add(0, ref_int ? i2f(wmul(new_inv, refi)) : i2f(new_inv) * ref, tick);  // inventoryValue
-    D.add(1, i2f(traded), i2f(wadd(traded, oq)));                              // market_share
-    D.add(2, i2f(inv) * (mid_end - X.wmid), tick);                             // InventoryPnL
-    D.add(3, ref, tick);                                                       // portfolio value's ref / tick
-    D.add(4, old_ref, tick);                                                   // the old net worth's
-    D.run();
-    const float inv_value = D.get(0);
-    const float net_worth = cash + inv_value;
-    const float market_share = D.get(1);
-    const float invPnL = D.get(2);
-    float buyPnL, sellPnL;
-    if (quiet) {  // (the rows' one signed zero: sign of the reference price term)
-        // (x / tick * +0 is the zero of x's sign: x finite, tick >= 1, |x| >= 1 or x = +-0)
-        const float zb = copysignf(0.0f, ref_int ? i2f(wsub(rbi, 0)) : ref_buy - i2f(0));
-        const float zs = copysignf(0.0f, ref_int ? i2f(wsub(0, rsi)) : i2f(0) - ref_sell);
-        buyPnL = zsum(zb, nT);
-        sellPnL = zsum(zs, nT);
-    } else {
-        float bpl[S], spl[S];
-#pragma unroll
-        for (int r = 0; r < S; ++r) {
-            if (ref_int) {
-                bpl[r] = i2f(wsub(rbi, bP[r])) / tick * i2f(iabs_(bQ[r]));
-                spl[r] = i2f(wsub(sP[r], rsi)) / tick * i2f(iabs_(sQ[r]));
-            } else {
-                bpl[r] = (ref_buy - i2f(bP[r])) / tick * i2f(iabs_(bQ[r]));
-                spl[r] = (i2f(sP[r]) - ref_sell) / tick * i2f(iabs_(sQ[r]));
+    // the reward values: only when the step's outputs are emitted (the state needs PnL, cash and the
+    // inventory).  One assignment block for both cases below: with an early return the compiler
+    // merged the two paths' stores to different fields of R into stores through a selected address,
+    // which puts R in scratch memory
+    float reward = 0.0f, r_pv = 0.0f, r_sp = 0.0f, r_spd = 0.0f, r_spad = 0.0f, r_spad2 = 0.0f, d_nw = 0.0f,
+          market_share = 0.0f, buyPnL = 0.0f, sellPnL = 0.0f, invPnL = 0.0f, inv_value = 0.0f;
+    if (full) {
+        float ref_buy, ref_sell, ref;
+        i32 rbi = 0, rsi = 0, refi = 0;
+        if (ri == HFTLOB_PRICE_MID_AVG) { ref_buy = ref_sell = ref = X.avg_mid; }
+        else if (ref_int) {
+            const bool far = ri == HFTLOB_PRICE_FAR_TOUCH;
+            rbi = sel(far, X.last_ba, X.last_bb);
+            rsi = sel(far, X.last_bb, X.last_ba);
+            refi = new_inv > 0 ? rbi : rsi;
+            ref_buy = i2f(rbi); ref_sell = i2f(rsi); ref = i2f(refi);
+        } else { ref_buy = ref_sell = ref = X.last_mid; }
+        const i32 traded = wadd(bq, sq);
+        const float mid_end = X.last_mid;
+        float old_ref;
+        if (ri == HFTLOB_PRICE_FAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_ba, X.old_last_bb));
+        else if (ri == HFTLOB_PRICE_NEAR_TOUCH) old_ref = i2f(sel(inv > 0, X.old_last_bb, X.old_last_ba));
+        else old_ref = X.wmid;
+        DivBatch D{lane_id()};
+        D.add(0, ref_int ? i2f(wmul(new_inv, refi)) : i2f(new_inv) * ref, tick);  // inventoryValue
+        D.add(1, i2f(traded), i2f(wadd(traded, oq)));                              // market_share
+        D.add(2, i2f(inv) * (mid_end - X.wmid), tick);                             // InventoryPnL
+        D.add(3, ref, tick);                                                       // portfolio value's ref / tick
+        D.add(4, old_ref, tick);                                                   // the old net worth's
+        D.run();
+        inv_value = D.get(0);
+        const float net_worth = cash + inv_value;
+        market_share = D.get(1);
+        invPnL = D.get(2);
+        if (quiet) {  // (the rows' one signed zero: sign of the reference price term)
+            // (x / tick * +0 is the zero of x's sign: x finite, tick >= 1, |x| >= 1 or x = +-0)
+            const float zb = copysignf(0.0f, ref_int ? i2f(wsub(rbi, 0)) : ref_buy - i2f(0));
+            const float zs = copysignf(0.0f, ref_int ? i2f(wsub(0, rsi)) : i2f(0) - ref_sell);
+            buyPnL = zsum(zb, nT);
+            sellPnL = zsum(zs, nT);
+        } else {
+            float bpl[S], spl[S];
+    #pragma unroll
+            for (int r = 0; r < S; ++r) {
+                if (ref_int) {
+                    bpl[r] = i2f(wsub(rbi, bP[r])) / tick * i2f(iabs_(bQ[r]));
+                    spl[r] = i2f(wsub(sP[r], rsi)) / tick * i2f(iabs_(sQ[r]));
+                } else {
+                    bpl[r] = (ref_buy - i2f(bP[r])) / tick * i2f(iabs_(bQ[r]));
+                    spl[r] = (i2f(sP[r]) - ref_sell) / tick * i2f(iabs_(sQ[r]));
+                }
             }
+            buyPnL = rows_fsum(bpl, nT);
+            sellPnL = rows_fsum(spl, nT);
         }
-        buyPnL = rows_fsum(bpl, nT);
-        sellPnL = rows_fsum(spl, nT);
-    }
-    const float eta = tc.inventoryPnL_eta, gam = tc.inventoryPnL_gamma;
-    const float r_sp = buyPnL + sellPnL + rebate_income + invPnL;
-    const float r_spd = buyPnL + sellPnL + rebate_income + invPnL - eta * invPnL;
-    const float r_spad = buyPnL + sellPnL + rebate_income + invPnL - fmaxf(0.0f, eta * invPnL);
-    const float r_spad2 = buyPnL + sellPnL + rebate_income + gam * (invPnL - fmaxf(0.0f, eta * invPnL));
-    const float r_sps = buyPnL + sellPnL + rebate_income + eta * (invPnL - tc.one_minus_eta * fmaxf(0.0f, invPnL));
-    float r_complex = 0.0f;
-    if (tc.reward_function == HFTLOB_MM_REW_COMPLEX) {
-        float abp[S], asp[S];
-#pragma unroll
-        for (int r = 0; r < S; ++r) {
-            abp[r] = i2f(bP[r]) / i2f(bq) * i2f(iabs_(bQ[r]));
-            asp[r] = i2f(sP[r]) / i2f(sq) * i2f(iabs_(sQ[r]));
+        const float eta = tc.inventoryPnL_eta, gam = tc.inventoryPnL_gamma;
+        r_sp = buyPnL + sellPnL + rebate_income + invPnL;
+        r_spd = buyPnL + sellPnL + rebate_income + invPnL - eta * invPnL;
+        r_spad = buyPnL + sellPnL + rebate_income + invPnL - fmaxf(0.0f, eta * invPnL);
+        r_spad2 = buyPnL + sellPnL + rebate_income + gam * (invPnL - fmaxf(0.0f, eta * invPnL));
+        const float r_sps = buyPnL + sellPnL + rebate_income + eta * (invPnL - tc.one_minus_eta * fmaxf(0.0f, invPnL));
+        float r_complex = 0.0f;
+        if (tc.reward_function == HFTLOB_MM_REW_COMPLEX) {
+            float abp[S], asp[S];
+    #pragma unroll
+            for (int r = 0; r < S; ++r) {
+                abp[r] = i2f(bP[r]) / i2f(bq) * i2f(iabs_(bQ[r]));
+                asp[r] = i2f(sP[r]) / i2f(sq) * i2f(iabs_(sQ[r]));
+            }
+            const float avg_buy = bq > 0 ? rows_fsum(abp, nT) : 0.0f;
+            const float avg_sell = sq > 0 ? rows_fsum(asp, nT) : 0.0f;
+            const i32 inv_change = wsub(bq, sq);
+            const float real_pnl = i2f(imin_(bq, sq)) * (avg_sell - avg_buy);
+            const float unreal = inv_change > 0 ? i2f(inv_change) * (X.avg_mid - avg_buy)
+                                                : i2f(iabs_(inv_change)) * (avg_sell - X.avg_mid);
+            r_complex = real_pnl + tc.unrealizedPnL_lambda * unreal + eta * fminf(invPnL, invPnL * eta);
         }
-        const float avg_buy = bq > 0 ? rows_fsum(abp, nT) : 0.0f;
-        const float avg_sell = sq > 0 ? rows_fsum(asp, nT) : 0.0f;
-        const i32 inv_change = wsub(bq, sq);
-        const float real_pnl = i2f(imin_(bq, sq)) * (avg_sell - avg_buy);
-        const float unreal = inv_change > 0 ? i2f(inv_change) * (X.avg_mid - avg_buy)
-                                            : i2f(iabs_(inv_change)) * (avg_sell - X.avg_mid);
-        r_complex = real_pnl + tc.unrealizedPnL_lambda * unreal + eta * fminf(invPnL, invPnL * eta);
+        r_pv = i2f(new_inv) * D.get(3) + cash;
+        const float old_nw = D.get(4) * i2f(inv) + bitf(st[4]);
+        d_nw = net_worth - old_nw;
+        switch (tc.reward_function) {
+            case HFTLOB_MM_REW_PORTFOLIO_VALUE: reward = r_pv; break;
+            case HFTLOB_MM_REW_BUY_SELL_PNL: reward = buyPnL + sellPnL; break;
+            case HFTLOB_MM_REW_COMPLEX: reward = r_complex; break;
+            case HFTLOB_MM_REW_ZERO_INV: reward = i2f(wsub(0, iabs_(new_inv))); break;
+            case HFTLOB_MM_REW_SPOONER: reward = r_sp; break;
+            case HFTLOB_MM_REW_SPOONER_DAMPED: reward = r_spd; break;
+            case HFTLOB_MM_REW_SPOONER_ASYM_DAMPED: reward = r_spad; break;
+            case HFTLOB_MM_REW_SPOONER_SCALED: reward = r_sps; break;
+            case HFTLOB_MM_REW_DELTA_PORTFOLIO_VALUE: reward = d_nw; break;
+            default: reward = r_spad2; break;
+        }
+        float inv_pen = 0.0f;
+        if (tc.inv_penalty == HFTLOB_INVPEN_LINEAR) inv_pen = i2f(wsub(0, iabs_(new_inv)));
+        else if (tc.inv_penalty == HFTLOB_INVPEN_QUADRATIC)
+            inv_pen = i2f(wmul(-1, wmul(new_inv, new_inv))) / tc.inv_penalty_quadratic_factor;
+        else if (tc.inv_penalty == HFTLOB_INVPEN_THRESHOLD)
+            inv_pen = i2f(iabs_(new_inv)) > tc.inv_penalty_threshold
+                          ? -1.0f * (i2f(wmul(new_inv, new_inv)) / tc.inv_penalty_quadratic_factor) : 0.0f;
+        else if (tc.inv_penalty == HFTLOB_INVPEN_EXP4)  // mm_env.py:2528-2529: -exp(inv * 4), int32 product
+            inv_pen = -1.0f * expf(i2f(wmul(new_inv, 4)));
+        reward = reward + tc.inv_penalty_lambda * inv_pen;
+        if (tc.clip_reward) reward = fminf(fmaxf(reward, -10000.0f), 10000.0f);
+        if (tc.volume_traded_bonus == 1) reward = reward + fabsf(reward) * market_share;
+        if (tc.exclude_extreme_spreads && excl_any) reward = 0.0f;
     }
-    const float r_pv = i2f(new_inv) * D.get(3) + cash;
-    const float old_nw = D.get(4) * i2f(inv) + bitf(st[4]);
-    const float d_nw = net_worth - old_nw;
-    float reward;
-    switch (tc.reward_function) {
-        case HFTLOB_MM_REW_PORTFOLIO_VALUE: reward = r_pv; break;
-        case HFTLOB_MM_REW_BUY_SELL_PNL: reward = buyPnL + sellPnL; break;
-        case HFTLOB_MM_REW_COMPLEX: reward = r_complex; break;
-        case HFTLOB_MM_REW_ZERO_INV: reward = i2f(wsub(0, iabs_(new_inv))); break;
-        case HFTLOB_MM_REW_SPOONER: reward = r_sp; break;
-        case HFTLOB_MM_REW_SPOONER_DAMPED: reward = r_spd; break;
-        case HFTLOB_MM_REW_SPOONER_ASYM_DAMPED: reward = r_spad; break;
-        case HFTLOB_MM_REW_SPOONER_SCALED: reward = r_sps; break;
-        case HFTLOB_MM_REW_DELTA_PORTFOLIO_VALUE: reward = d_nw; break;
-        default: reward = r_spad2; break;
-    }
-    float inv_pen = 0.0f;
-    if (tc.inv_penalty == HFTLOB_INVPEN_LINEAR) inv_pen = i2f(wsub(0, iabs_(new_inv)));
-    else if (tc.inv_penalty == HFTLOB_INVPEN_QUADRATIC)
-        inv_pen = i2f(wmul(-1, wmul(new_inv, new_inv))) / tc.inv_penalty_quadratic_factor;
-    else if (tc.inv_penalty == HFTLOB_INVPEN_THRESHOLD)
-        inv_pen = i2f(iabs_(new_inv)) > tc.inv_penalty_threshold
-                      ? -1.0f * (i2f(wmul(new_inv, new_inv)) / tc.inv_penalty_quadratic_factor) : 0.0f;
-    else if (tc.inv_penalty == HFTLOB_INVPEN_EXP4)  // mm_env.py:2528-2529: -exp(inv * 4), int32 product
-        inv_pen = -1.0f * expf(i2f(wmul(new_inv, 4)));
-    reward = reward + tc.inv_penalty_lambda * inv_pen;
-    if (tc.clip_reward) reward = fminf(fmaxf(reward, -10000.0f), 10000.0f);
-    if (tc.volume_traded_bonus == 1) reward = reward + fabsf(reward) * market_share;
-    if (tc.exclude_extreme_spreads && excl_any) reward = 0.0f;
     R.reward = reward; R.reward_pv = r_pv; R.reward_spooner = r_sp; R.end_of_ep_pv = r_pv * (float)X.ep_done;
     R.reward_spooner_damped = r_spd; R.reward_spooner_asym_damped = r_spad; R.reward_spooner_asym_damped2 = r_spad2;
-    R.reward_delta_pv = d_nw; R.market_share = market_share; R.delta_mid = mid_end - X.wmid; R.buyPnL = buyPnL;
+    R.reward_delta_pv = d_nw; R.market_share = market_share; R.delta_mid = X.last_mid - X.wmid; R.buyPnL = buyPnL;
     R.sellPnL = sellPnL; R.invPnL = invPnL; R.PnL = PnL; R.cash = cash; R.inventoryValue = inv_value;
     R.end_inventory = new_inv;
     (void)M;
@@ -2733,9 +2735,11 @@ template <int S> DEV void write_debug(const Book<S>& B, i32* dst) {
 #define MAX_AGENT_ROWS 128
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
-template <int S, int NFIX, bool RC, bool RA = false>
+template <int S, int NFIX, bool RC, bool RA = false, bool QUIET = false>
 // RC: cancel_mode 2/3 (the random cancel fallback of the engine).  RA: the agent rows live in the
-// trade log (lds_map).
+// trade log (lds_map).  QUIET: a step whose outputs are never emitted (emit = false at compile
+// time: k_env_rollout's per_step = 0 steps before the last, whose copy of the step body then holds
+// no observation or reward-value code).
 // master: Speed_test rollout mode — the env's step key is split(mk, n_env + 1)[e + 1],
 // actions are sampled here (hftlob_sample_actions) and written to actions_io if it is not
 // NULL; mk becomes split(mk)[0].  Otherwise keys / actions_io are the inputs.  (mk is a
@@ -2755,7 +2759,8 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                       float* __restrict__ rew_out, u8* __restrict__ done_all_out, u8* __restrict__ dones_out,
                       i32* __restrict__ info_out, i32* __restrict__ obs_raw_out, i32* __restrict__ msgs_out,
                       i32* __restrict__ debug_out, i32* lds, bool resident, bool keep, u32& fl_carry,
-                      const i32* pre_keys = nullptr, bool emit = true) {
+                      const i32* pre_keys = nullptr, bool emit_rt = true) {
+    const bool emit = !QUIET && emit_rt;
     STAMP(t_start);
 #ifdef HFTLOB_STAMPS
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz: the in-kernel clock
@@ -3353,8 +3358,13 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
     const bool kbat = kb_ok(c);
     const int kbw = kb_words(c);
     i32* kbuf = lds + lds_map(c, NFIX > 0 ? NFIX : c.lob.n_orders, NFIX > 0 ? NFIX : c.lob.n_trades, RA).kb;
-#pragma unroll 1
-    for (int t = 0; t < n_steps; ++t) {
+    // one step of the rollout: Q = true for a step whose outputs are not emitted (per_step = 0, not
+    // the last step).  The quiet steps run in a loop of their own, then the emitted ones (per_step =
+    // 1: all steps; 0: the last one) in a second loop: the quiet copy of the step body holds no
+    // observation / reward-value code, and the constants the emitting copy keeps in registers are
+    // not live across the quiet loop
+    auto step = [&](auto Q, int t) {
+        constexpr bool QT = decltype(Q)::value;
         const size_t o = per_step ? (size_t)t * n_env : 0;
         const int tb = t % KB_STEPS;
         kcfg_t* cp = kp;
@@ -3366,17 +3376,15 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         STAMP(kb0);
         if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
         STAMP(kb1);
-        // per_step = 0: only the last step's outputs are written (env_step_dev's emit)
-        const bool emit = (per_step != 0) | (t + 1 == n_steps);
-        const bool ox = emit;  // (the optional outputs: written by the emitted steps only)
-        const bool reset = env_step_dev<S, NFIX, RC, RA>(
+        const bool ox = !QT;  // (the optional outputs: written by the emitted steps only)
+        const bool reset = env_step_dev<S, NFIX, RC, RA, QT>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
             out.dones + o * cc.n_agents, ox && out.info ? out.info + o * cc.info_words : nullptr,
             ox && out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
             ox && out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr,
             ox && out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds,
-            NFIX > 0 && resident, NFIX > 0 && t + 1 < n_steps, fl, kbat ? kbuf + tb * kbw : nullptr, emit);
+            NFIX > 0 && resident, NFIX > 0 && t + 1 < n_steps, fl, kbat ? kbuf + tb * kbw : nullptr, !QT);
         resident = uni(!reset) != 0;  // (uniform: the divergence analysis cannot see it through the reset's lane loops)
         STAMP(bp0);
 #ifndef HFTLOB_NO_BALANCE
@@ -3407,7 +3415,14 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
             if (lane_id() < 10) out.info[((size_t)t * n_env + e) * cc.info_words + lane_id()] = v;
         }
 #endif
+    };
+    int t = 0;
+    if (!per_step) {
+#pragma unroll 1
+        for (; t + 1 < n_steps; ++t) step(std::integral_constant<bool, true>{}, t);
     }
+#pragma unroll 1
+    for (; t < n_steps; ++t) step(std::integral_constant<bool, false>{}, t);
 #ifndef HFTLOB_NO_BALANCE
     // the wave is done: its slot's entry becomes a past time, so no neighbour counts it as live
     if (lane_id() == 0) __hip_atomic_store(bal_row + bal_slot, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
