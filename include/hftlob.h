@@ -347,10 +347,13 @@ int hftlob_env_lds_bytes(const hftlob_env_cfg* cfg /*[host]*/);
  *                 raises the envs a CU holds, e.g. Speed_test's [5, 5] agents)
  *   lds_bytes     dynamic LDS per env workgroup (hftlob_env_lds_bytes)
  *   tick_magic    the multiplier of the exact floor division by tick_size the kernels use,
- *                 ceil(2^(31+l) / tick_size), l = ceil(log2 tick_size) */
+ *                 ceil(2^(31+l) / tick_size), l = ceil(log2 tick_size)
+ *   key_batch     1: hftlob_env_rollout_sampled's persistent launch derives the step keys four
+ *                 steps at a time (partitionable keys, <= 3 agents, <= 8 action rows) */
 typedef struct hftlob_launch_info {
     int32_t slot_sets, nfix, random_cancel, rows_alias, lds_bytes;
     uint32_t tick_magic;
+    int32_t key_batch;
 } hftlob_launch_info;
 int hftlob_env_launch_info(const hftlob_env_cfg* cfg /*[host]*/, hftlob_launch_info* out /*[host]*/);
 

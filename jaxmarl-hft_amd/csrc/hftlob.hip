@@ -2592,14 +2592,17 @@ __host__ __device__ inline bool kb_ok(const hftlob_env_cfg& c) {  // (a step's r
 }
 __host__ __device__ inline int kb_words(const hftlob_env_cfg& c) { return 6 + c.n_agents + c.n_action_msgs; }
 // LDS carve-up of one env's workgroup (words): [agent rows (C+A)*8][action extras][book: asks 6nO,
-// bids 6nO, trades 8nT, pad 256][key batches].  When the agent rows all fall in the first message
-// chunk (C + A <= 64) and fit the trade log's rows (C + A <= nT), they can live IN the trade log
-// instead: it is free from the step's start until trades_fill, which then runs after chunk 0's
-// rows are read.  (Speed_test's [5,5] agents: 60 rows, 1.9 KB less per env, 16 envs per CU
-// instead of 14.)
+// bids 6nO, trades 8nT, pad 256][key batches].  The agent rows can live IN the trade log instead:
+// it is free from the step's start until trades_fill, which then runs once the rows are read.
+// (Speed_test's [5,5] agents: 60 rows, 1.9 KB less per env, 16 envs per CU instead of 14.)
+// The rows may span two message chunks (C + A <= 128): the second chunk's agent rows are read into
+// its registers with the first chunk's, before trades_fill.  They may run past the trade log into
+// the pad's over-read area and filter words (both unused until chunk 0's rows are read), not into
+// its scratch row (filter_rows' scratch): (C + A) * 8 <= 8 nT + 192 words.  (Speed_test's [10, 10]
+// agents: 120 rows at nT = 100.)
 __host__ __device__ inline bool rows_in_trades(const hftlob_env_cfg& c, int nT) {
     const int ar = c.n_cancel_msgs + c.n_action_msgs;
-    return ar <= 64 && ar <= nT;
+    return ar <= 128 && 8 * ar <= 8 * nT + 192;
 }
 struct LdsMap {
     int rows, axs, book, kb, words;  // word offsets, total words
@@ -2735,11 +2738,12 @@ template <int S> DEV void write_debug(const Book<S>& B, i32* dst) {
 #define MAX_AGENT_ROWS 128
 // NFIX > 0: nOrders == nTrades == NFIX known at compile time (the reference's
 // 100/100 default), which folds the slot-validity masks away.
-template <int S, int NFIX, bool RC, bool RA = false, bool QUIET = false>
+template <int S, int NFIX, bool RC, bool RA = false, bool QUIET = false, int PK = -1>
 // RC: cancel_mode 2/3 (the random cancel fallback of the engine).  RA: the agent rows live in the
 // trade log (lds_map).  QUIET: a step whose outputs are never emitted (emit = false at compile
 // time: k_env_rollout's per_step = 0 steps before the last, whose copy of the step body then holds
-// no observation or reward-value code).
+// no observation or reward-value code).  PK: 1 = the step's keys always come from a key-batch row
+// (pre_keys, k_env_rollout's KB = 1), 0 = never, -1 = as pre_keys is given.
 // master: Speed_test rollout mode — the env's step key is split(mk, n_env + 1)[e + 1],
 // actions are sampled here (hftlob_sample_actions) and written to actions_io if it is not
 // NULL; mk becomes split(mk)[0].  Otherwise keys / actions_io are the inputs.  (mk is a
@@ -2788,8 +2792,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     const bool agw_pre = naw <= 64;
     const i32 agw = (agw_pre & (l < naw)) ? rec[c.off_agents + l] : 0;
     // (pre_keys: this step's row of a k_env_rollout key batch, step_keys_batch)
-    const StepKeys SK = pre_keys ? load_keys(c, pre_keys) : step_keys<NFIX == 0>(c, key_n, ek, keys, master, mk);
-    if (master && !pre_keys) mk = SK.next_master;
+    const bool batched = PK == 1 || (PK < 0 && pre_keys);
+    const StepKeys SK = batched ? load_keys(c, pre_keys) : step_keys<NFIX == 0>(c, key_n, ek, keys, master, mk);
+    if (master && !batched) mk = SK.next_master;
     const Key key_reset = SK.key_reset;
     if (RC) {  // the scan's key: k1, or split(k1)[0] after the shuffle split (marl_env.py:293-294,349-351)
         B.ek = c.shuffle_action_messages ? split_key(SK.k1, 2, 0, c.prng_partitionable) : SK.k1;
@@ -3017,10 +3022,10 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     for (int base = 0; base < M; base += 64) {
         const int row = base + l;
         int4 x = nx, y = ny;
-        if (row < AR) {
+        if (RA ? (base == 0) & (row < AR) : row < AR) {  // (RA: chunk 1's agent rows came with chunk 0's)
             x = reinterpret_cast<const int4*>(rows + row * 8)[0];
             y = reinterpret_cast<const int4*>(rows + row * 8)[1];
-        } else if (ftime && base > 0) {
+        } else if (ftime && base > 0 && row >= AR) {
             fixed_time_mask(x, y, t_end);
         }
         if (msgs_out && row < M) {  // the combined message row as the book receives it ("messages" obs)
@@ -3035,8 +3040,12 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             nx = reinterpret_cast<const int4*>(g)[0];
             ny = reinterpret_cast<const int4*>(g)[1];
         }
-        if (RA && (base == 0)) {  // the step's trade log starts all -1: reset once chunk 0's agent rows,
-            lds_order();          // which live in it, are read (a wave's LDS operations run in order)
+        if (RA && (base == 0)) {  // the step's trade log starts all -1: reset once the agent rows, which
+            if (row + 64 < AR) {  // live in it, are read (chunk 1's into its registers; a wave's LDS
+                nx = reinterpret_cast<const int4*>(rows + (row + 64) * 8)[0];  // operations run in order)
+                ny = reinterpret_cast<const int4*>(rows + (row + 64) * 8)[1];
+            }
+            lds_order();
             trades_fill(B.tr, B.vt, -1);
         }
         decode_msgs(B.c, x, y);
@@ -3323,7 +3332,10 @@ DEV void balance_prio(unsigned long long* row, u32 slot, unsigned long long r0, 
     else if (q == 2) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
 }
-template <int S, int NFIX, bool RC, bool RA = false>
+// KB: 1 = the config derives its step keys in batches (kb_ok, checked by the launch code), 0 = it
+// does not, -1 = decided at run time (the general-size and rows-alias instantiations).  The metric
+// kernel is KB = 1: its loop holds no per-step key derivation.
+template <int S, int NFIX, bool RC, bool RA = false, int KB = -1>
 __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_env, int key_e0, int key_n, int n_steps,
                                                     int per_step, const u32* __restrict__ master,
                                                     u32* __restrict__ master_out, i32* __restrict__ actions_io,
@@ -3355,7 +3367,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
     const u32 wt_hwid = __builtin_amdgcn_s_getreg(0xF804), wt_xcc = __builtin_amdgcn_s_getreg(0x7814);
 #endif
     // the key batches (step_keys_batch) live after the book in LDS
-    const bool kbat = kb_ok(c);
+    const bool kbat = KB < 0 ? kb_ok(c) : KB == 1;
     const int kbw = kb_words(c);
     i32* kbuf = lds + lds_map(c, NFIX > 0 ? NFIX : c.lob.n_orders, NFIX > 0 ? NFIX : c.lob.n_trades, RA).kb;
     // one step of the rollout: Q = true for a step whose outputs are not emitted (per_step = 0, not
@@ -3377,7 +3389,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
         STAMP(kb1);
         const bool ox = !QT;  // (the optional outputs: written by the emitted steps only)
-        const bool reset = env_step_dev<S, NFIX, RC, RA, QT>(
+        const bool reset = env_step_dev<S, NFIX, RC, RA, QT, KB>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
             out.dones + o * cc.n_agents, ox && out.info ? out.info + o * cc.info_words : nullptr,
@@ -3472,7 +3484,7 @@ __global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__
                          hftlob_step_out
 #define HFTLOB_STEP(P, SS, NF, RC) P template __global__ void k_env_step<SS, NF, RC, false>(HFTLOB_STEP_ARGS);
 #define HFTLOB_ROLL(P, SS, NF, RC) P template __global__ void k_env_rollout<SS, NF, RC, false>(HFTLOB_ROLL_ARGS);
-#define HFTLOB_PART1(P) HFTLOB_ROLL(P, 2, 100, false)
+#define HFTLOB_PART1(P) P template __global__ void k_env_rollout<2, 100, false, false, 1>(HFTLOB_ROLL_ARGS);
 #define HFTLOB_PART2(P) HFTLOB_STEP(P, 2, 100, false)
 #define HFTLOB_PART3(P) HFTLOB_ROLL(P, 1, 0, false) HFTLOB_STEP(P, 1, 0, false)
 #define HFTLOB_PART4(P) HFTLOB_ROLL(P, 2, 0, false) HFTLOB_STEP(P, 2, 0, false)
@@ -3481,6 +3493,7 @@ __global__ void k_split_keys(int n_env, int n, int part, const u32* __restrict__
 #define HFTLOB_PART7(P) HFTLOB_STEP(P, 2, 0, true) HFTLOB_ROLL(P, 4, 0, true) HFTLOB_STEP(P, 4, 0, true)
 #define HFTLOB_PART8(P) P template __global__ void k_env_rollout<2, 100, false, true>(HFTLOB_ROLL_ARGS); \
                         P template __global__ void k_env_step<2, 100, false, true>(HFTLOB_STEP_ARGS);
+#define HFTLOB_PART9(P) P template __global__ void k_env_rollout<2, 100, false, false, 0>(HFTLOB_ROLL_ARGS);
 #define HFTLOB_NONE
 #if defined(HFTLOB_INST)
 #if HFTLOB_INST == 1
@@ -3499,11 +3512,13 @@ HFTLOB_PART6(HFTLOB_NONE)
 HFTLOB_PART7(HFTLOB_NONE)
 #elif HFTLOB_INST == 8
 HFTLOB_PART8(HFTLOB_NONE)
+#elif HFTLOB_INST == 9
+HFTLOB_PART9(HFTLOB_NONE)
 #endif
 #else  // the main translation unit
 #if !defined(HFTLOB_SINGLE_TU)
 HFTLOB_PART1(extern) HFTLOB_PART2(extern) HFTLOB_PART3(extern) HFTLOB_PART4(extern)
-HFTLOB_PART5(extern) HFTLOB_PART6(extern) HFTLOB_PART7(extern) HFTLOB_PART8(extern)
+HFTLOB_PART5(extern) HFTLOB_PART6(extern) HFTLOB_PART7(extern) HFTLOB_PART8(extern) HFTLOB_PART9(extern)
 #endif
 
 // ================================================================ C ABI
@@ -3717,7 +3732,11 @@ static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, 
         if (use_rows_alias(cfg)) hipLaunchKernelGGL((k_env_rollout<2, 100, false, true>), g, b, shm, st, kc, n_env,
                                                     key_e0, key_n, n_steps, per_step, key_in, key_out, actions, msg_data,
                                                     init_states, state, *out);
-        else LAUNCH_ROLL(2, 100, false);
+        else if (kb_ok(*cfg)) hipLaunchKernelGGL((k_env_rollout<2, 100, false, false, 1>), g, b, shm, st, kc, n_env, key_e0,
+                                                 key_n, n_steps, per_step, key_in, key_out, actions, msg_data,
+                                                 init_states, state, *out);
+        else hipLaunchKernelGGL((k_env_rollout<2, 100, false, false, 0>), g, b, shm, st, kc, n_env, key_e0, key_n, n_steps,
+                                per_step, key_in, key_out, actions, msg_data, init_states, state, *out);
     }
     else if (S == 1) LAUNCH_ROLL(1, 0, false);
     else if (S == 2) LAUNCH_ROLL(2, 0, false);
@@ -3828,6 +3847,7 @@ int hftlob_env_launch_info(const hftlob_env_cfg* cfg, hftlob_launch_info* out) {
     out->rows_alias = nf && use_rows_alias(cfg) ? 1 : 0;
     out->lds_bytes = (int)env_shm(cfg);
     out->tick_magic = kernel_cfg(cfg).tick_magic;
+    out->key_batch = kb_ok(*cfg) ? 1 : 0;
     return HFTLOB_OK;
 }
 

@@ -15,7 +15,8 @@ from .layout import EnvCfg, LobCfg, StepOut
 class LaunchInfo(C.Structure):
     """hftlob_launch_info (include/hftlob.h): the kernel instantiation a config launches."""
     _fields_ = [("slot_sets", C.c_int32), ("nfix", C.c_int32), ("random_cancel", C.c_int32),
-                ("rows_alias", C.c_int32), ("lds_bytes", C.c_int32), ("tick_magic", C.c_uint32)]
+                ("rows_alias", C.c_int32), ("lds_bytes", C.c_int32), ("tick_magic", C.c_uint32),
+                ("key_batch", C.c_int32)]
 
 LIB_PATH = os.environ.get("HFTLOB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhftlob.so")
 ABI_VERSION = 7

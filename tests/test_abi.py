@@ -154,7 +154,7 @@ def test_env_lds_bytes(L, name, agents, part, kb):
     MARLEnv.resident_envs sizes launch shapes from) on both sides of the rollout's key-batch rule
     (kb_ok: partitionable keys, <= 3 agents, <= 8 action rows, 6 + agents + rows <= 16):
     [rows (C+A)*8][action extras][asks 6 nO][bids 6 nO][trades 8 nT][pad 64*4][key batches 4 x row], the
-    rows inside the trade log for Speed_test's [5,5] (16 envs per CU instead of 14)."""
+    rows inside the trade log for Speed_test's [5,5] and [10,10] (16 envs per CU instead of 14 / 11)."""
     import dataclasses
     cfg = builtin_config(name)
     if agents:
@@ -168,14 +168,16 @@ def test_env_lds_bytes(L, name, agents, part, kb):
                 + (4 * (6 + c.n_agents + c.n_action_msgs) if kb else 0))
     # the agent rows live in the trade log (lds_map, use_rows_alias) only in the 100/100 kernel, when
     # they fit and their own region would hold the env above 160 KB / 16
-    alias = (c.lob.n_orders == c.lob.n_trades == 100 and c.lob.cancel_mode < 2 and ar <= 64
-             and ar <= c.lob.n_trades and rest + 4 * ar * 8 > 160 * 1024 // 16)
-    assert alias == (agents == [5, 5])
+    # (rows_in_trades: at most two message chunks of rows, ending before the pad's scratch row)
+    alias = (c.lob.n_orders == c.lob.n_trades == 100 and c.lob.cancel_mode < 2 and ar <= 128
+             and 8 * ar <= 8 * c.lob.n_trades + 192 and rest + 4 * ar * 8 > 160 * 1024 // 16)
+    assert alias == (agents in ([5, 5], [10, 10]))
     assert L.hftlob_env_lds_bytes(C.byref(c)) == rest + (0 if alias else 4 * ar * 8)
     info = _lib.LaunchInfo()
     assert L.hftlob_env_launch_info(C.byref(c), C.byref(info)) == 0
     assert (info.slot_sets, info.nfix, info.random_cancel, info.rows_alias) == (2, 100, 0, int(alias))
     assert info.lds_bytes == L.hftlob_env_lds_bytes(C.byref(c))
+    assert info.key_batch == int(kb)
     c.ep_type = 2
     assert L.hftlob_env_lds_bytes(C.byref(c)) == -1   # an invalid cfg: its error code
     assert L.hftlob_env_launch_info(C.byref(c), C.byref(info)) == -1

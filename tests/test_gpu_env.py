@@ -408,6 +408,8 @@ def _named_config(name):
                                                           ("speed_5_5", True, None, 70, False, 0),
                                                           ("speed_5_5", True, None, 7, True, 0),
                                                           ("speed_5_5", False, None, 9, True, 0),
+                                                          ("speed_10_10", True, None, 70, False, 0),
+                                                          ("speed_10_10", True, None, 7, True, 0),
                                                           ("2_player_fq_fqc", True, None, 7, True, 0),
                                                           ("3_player_fq_fqc_dir", False, None, 13, True, 0),
                                                           ("exec_debug_fixed_quants_complex", False, 2, 9, True, 0),
@@ -426,7 +428,7 @@ def test_rollout_sampled_equals_step_sampled(name, part, exe, T, per_step, G):
         cfg = variant(cfg, "Execution", action_space="fixed_prices", n_actions=exe, fixed_quant_value=11)
     w = cfg.world_config
     env = MARLEnv(None, cfg, data=_day(w, 2_000_000), prng_partitionable=part)
-    if name.startswith("speed_5_5"):  # the rows-alias instantiation (k_env_rollout<2, 100, false, true>)
+    if name.startswith("speed_"):  # the rows-alias instantiation (k_env_rollout<2, 100, false, true>)
         assert env.launch_info()["rows_alias"] == 1
     params = env.default_params
     E = 40
@@ -575,20 +577,23 @@ def test_speed_test_sweep_parity(agents, D):
     assert (k_out.cpu().numpy().view(np.uint32) == o_key).all(), "carried key"
 
 
-@pytest.mark.parametrize("D,E", [(100, 24), (1, 24), (100, 4000), (1, 4000)])
-def test_speed_test_rows_alias_persistent(D, E):
-    """Speed_test's [5, 5] agents at their default launch: ONE persistent k_env_rollout launch of the
-    rows-alias instantiation (k_env_rollout<2, 100, false, true>: the 60 agent message rows live
-    inside the trade log, trades_fill after chunk 0, the book resident in LDS from step to step),
+@pytest.mark.parametrize("agents,D,E", [([5, 5], 100, 24), ([5, 5], 1, 24), ([5, 5], 100, 4000), ([5, 5], 1, 4000),
+                                        ([10, 10], 100, 24), ([10, 10], 1, 24), ([10, 10], 100, 4000),
+                                        ([10, 10], 1, 4000)], ids=lambda x: str(x))
+def test_speed_test_rows_alias_persistent(agents, D, E):
+    """Speed_test's [5, 5] and [10, 10] agents at their default launch: ONE persistent k_env_rollout
+    launch of the rows-alias instantiation (k_env_rollout<2, 100, false, true>: the 60 / 120 agent
+    message rows live inside the trade log, [10, 10]'s over two message chunks whose second is read
+    into registers with the first, trades_fill after that, the book resident in LDS from step to step),
     at 24 envs and at the sweep's 4000 envs, 70 steps over 32-step episodes so every env crosses
     two auto-resets; end state and carried master key against the oracle's C rollout loop
     (Speed_test.py:50-71,186-196).  hftlob_env_launch_info asserts the instantiation."""
-    cfg = speed_test_config([5, 5], D)
+    cfg = speed_test_config(agents, D)
     env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000), return_info=False, persistent_outputs=True)
     info = env.launch_info()
     assert (info["nfix"], info["rows_alias"], info["random_cancel"]) == (100, 1, 0)
     assert info["lds_bytes"] == env.lds_bytes_per_env() and info["lds_bytes"] * 16 <= env.LDS_PER_CU
-    assert env.default_slices(E) == 0, "the [5, 5] default launch is the persistent one"
+    assert env.default_slices(E) == 0, "the default launch is the persistent one"
     params = env.default_params
     T = 70
     keys = split_keys(torch.zeros((1, 2), dtype=torch.int32, device="cuda"), E + 1)[0]
@@ -599,7 +604,7 @@ def test_speed_test_rows_alias_persistent(D, E):
     torch.cuda.synchronize()
     o_st, o_key = O.rollout_sampled(env.cfg_c, kin.cpu().numpy().view(np.uint32), env.data.msgs,
                                     env._init_states.cpu().numpy(), s0, T)
-    _compare_state(env, o_st, state.buf.cpu().numpy(), f"[5,5] x {D} persistent rollout, {E} envs")
+    _compare_state(env, o_st, state.buf.cpu().numpy(), f"{agents} x {D} persistent rollout, {E} envs")
     assert (kout.cpu().numpy().view(np.uint32) == o_key).all(), "carried key"
     assert (state.world_state.step_counter.cpu().numpy() < T).all(), "every env crossed its episode end"
 

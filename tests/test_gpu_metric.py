@@ -154,20 +154,18 @@ def test_c4_shards_compose_at_real_size():
 def test_default_launch_shape():
     """MARLEnv.default_slices: the persistent launch while its waves of workgroups are full (the
     metric: 4096 envs at 16 per CU, and whole multiples of it), 2 env slices when the last wave
-    would be partly empty (Speed_test's [10, 10] agents at 4000 envs, 11 envs per CU;
-    profiles/r03_launch_shape_sweep.txt, r04_speed_test_sweep.json)."""
+    would be partly empty (6000 envs; profiles/r03_launch_shape_sweep.txt, r04_speed_test_sweep.json)."""
     cfg = builtin_config("2_player_fq_fqc")
     env = MARLEnv(None, cfg, data=_day(cfg.world_config, 2_000_000))
     assert env.lds_bytes_per_env() * 16 <= env.LDS_PER_CU
     assert env.default_slices(4096) == 0 and env.default_slices(512) == 0
     assert env.default_slices(8192) == 0 and env.default_slices(16384) == 0
     assert env.default_slices(6000) == 2
-    # Speed_test's [5, 5] agents: 60 agent rows inside the trade log (lds_map), 16 envs per CU, so 4000
-    # envs are resident; [10, 10]: 120 rows (two chunks) in their own LDS, 11 envs per CU
-    big = dataclasses.replace(builtin_config("default"), number_of_agents_per_type=[5, 5])
-    env5 = MARLEnv(None, big, data=_day(big.world_config, 2_000_000))
-    assert env5.lds_bytes_per_env() * 16 <= env5.LDS_PER_CU
-    assert env5.default_slices(4000) == 0
-    big10 = dataclasses.replace(builtin_config("default"), number_of_agents_per_type=[10, 10])
-    env10 = MARLEnv(None, big10, data=_day(big10.world_config, 2_000_000))
-    assert env10.default_slices(4000) == 2
+    # Speed_test's [5, 5] / [10, 10] agents: 60 / 120 agent rows inside the trade log (lds_map; [10, 10]'s
+    # span two message chunks), 16 envs per CU, so 4000 envs are resident: one persistent launch
+    for ag in ([5, 5], [10, 10]):
+        big = dataclasses.replace(builtin_config("default"), number_of_agents_per_type=ag)
+        envb = MARLEnv(None, big, data=_day(big.world_config, 2_000_000))
+        assert envb.launch_info()["rows_alias"] == 1
+        assert envb.lds_bytes_per_env() * 16 <= envb.LDS_PER_CU
+        assert envb.default_slices(4000) == 0
