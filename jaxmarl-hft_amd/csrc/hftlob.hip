@@ -708,13 +708,16 @@ template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) 
         s.top_ts = t; s.top_tns = tns;
     }
 }
-template <bool BID, int S>
+// STALE_OK = false: the caller knows the side is not stale (add_free: no message starts with a
+// stale side, run_chunk refreshes both after each one, and an add without eviction changes only
+// the other side before it gets here)
+template <bool BID, int S, bool STALE_OK = true>
 DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint) {
     // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
     // common case, an order behind the best (one compare each); per side the cases are those of
     // get_best_* with -1 (and, for asks, maxint) standing for "no price".
     constexpr u32 STALE = SideBits<!BID>::STALE;
-    if (fl & STALE) { s.top = -1; return; }
+    if (STALE_OK && (fl & STALE)) { s.top = -1; return; }
     const i32 bp = s.best_p;
     if (BID) {
         if (np < bp) {
@@ -832,7 +835,7 @@ template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s,
     // does not cross (the loop's own first test, with an empty ask side standing for maxint)
     // (fresh: the RARE / common handler copies each keep their own test, not one shared lane mask)
     if (fresh(qtm) <= 0) return qtm;
-    if (B.fl & SideBits<!BID>::STALE) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+    // (no stale side here: run_chunk refreshes both sides after every message)
     {
         const i32 bp = s.best_p;
         const i32 mp0 = (!BID && bp == -1) ? B.c.maxint : bp;
@@ -980,12 +983,13 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
     }
-    note_add<BID>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
+    note_add<BID, S, false>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
 // tests are compiled out of the common FAST add
 template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
+    if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
     if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
     lmask free[S];
@@ -1001,6 +1005,7 @@ template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
 }
 // ask_lim — :446-508
 template <bool G, bool RARE, int S> DEV void ask_lim(Book<S>& B, Msg m) {
+    if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = 0;
     const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
     lmask free[S];
@@ -1145,6 +1150,7 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     if (p_add == -1) h |= H_PM1;  // an add would write an order priced -1
     if (c.t4 == 2) h |= H_MKT;    // type_4_interpretation MKT: the limit handlers' price overrides
     if (h & (H_DISCARD | H_NEG1 | H_PM1 | H_MKT)) h |= H_RARE;
+    if ((h <= H_BID) & (x.z <= 0)) h |= H_RARE;  // an add of no quantity (the common add handlers assume qty > 0)
     x.x = h;
     x.y = sd;
 }
@@ -3389,10 +3395,16 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
         if (kbat && tb == 0) step_keys_batch<NFIX == 0>(cc, key_n, key_e0 + e, mk, imin_(KB_STEPS, n_steps - t), kbuf);
         STAMP(kb1);
         const bool ox = !QT;  // (the optional outputs: written by the emitted steps only)
+#ifdef HFTLOB_STAMPS_QUIET
+        // diagnostic build only: the quiet steps' phase stamps go to their per_step info rows
+        const bool ox_info = true;
+#else
+        const bool ox_info = ox;
+#endif
         const bool reset = env_step_dev<S, NFIX, RC, RA, QT, KB>(
             cc, key_n, key_e0 + e, e, nullptr, true, mk, actions_io ? actions_io + o * cc.action_words : nullptr, md,
             is, st, out.obs + o * cc.n_agents * cc.obs_stride, out.rewards + o * cc.n_agents, out.done_all + o,
-            out.dones + o * cc.n_agents, ox && out.info ? out.info + o * cc.info_words : nullptr,
+            out.dones + o * cc.n_agents, ox_info && out.info ? out.info + o * cc.info_words : nullptr,
             ox && out.obs_raw ? out.obs_raw + o * cc.n_agents * cc.obs_stride : nullptr,
             ox && out.msgs ? out.msgs + o * cc.n_msgs * 8 : nullptr,
             ox && out.debug ? out.debug + o * (size_t)HFTLOB_DEBUG_WORDS(cc.lob.n_trades) : nullptr, lds,
@@ -3429,7 +3441,11 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
 #endif
     };
     int t = 0;
+#ifdef HFTLOB_STAMPS_QUIET  // diagnostic build only: per_step = 1 rollouts run the quiet body too (stamps of the bench's path)
+    if (true) {
+#else
     if (!per_step) {
+#endif
 #pragma unroll 1
         for (; t + 1 < n_steps; ++t) step(std::integral_constant<bool, true>{}, t);
     }

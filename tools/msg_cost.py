@@ -15,7 +15,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "jaxmarl-hft_amd")]
 
 import numpy as np  # noqa: E402
 
-KINDS = ["noop", "cancel_partial", "add_then_delete", "add_then_cross", "exec_ioc", "mixed_random"]
+KINDS = ["noop", "cancel_partial", "add_then_delete", "add_then_cross", "exec_ioc", "mixed_random", "full_add",
+         "cancel_wrap"]
+FULL = ("full_add", "cancel_wrap")  # run on a book whose sides hold 100 orders each (every add evicts)
 E, N = 4096, 448
 
 
@@ -38,6 +40,12 @@ def stream(kind, rng):
             row = (1, -1, 5, 1005, 5000 + j, 7, t, tn) if k % 2 == 0 else (1, 1, 5, 1005, 9000 + j, 8, t, tn)
         elif kind == "exec_ioc":
             row = (4, s, 1, 990 if s == 1 else 1010, 0, 7, t, tn)   # executes the touch (side flipped)
+        elif kind == "full_add":  # a limit order into a full side: check_book_fill evicts the worst level
+            p = (985 - int(rng.integers(0, 60))) if s == 1 else (1015 + int(rng.integers(0, 60)))
+            row = (1, s, int(rng.integers(1, 50)), p, 30000 + k, 7, t, tn)
+        elif kind == "cancel_wrap":  # an id no row holds, no init-id row at its price: the -1 index wraps to
+            p = 500 if s == 1 else 1500  # the last slot, which holds an order (partial cancel of it)
+            row = (2, s, 1, p, 70000 + k, 7, t, tn)
         else:
             u = rng.random()
             if u < 0.45:
@@ -66,9 +74,16 @@ def run():
     bids, trades = torch.full_like(asks, -1), torch.full((E, w.nTrades, 8), -1, dtype=torch.int32, device=dev)
     book_process_(w, torch.from_numpy(np.broadcast_to(init, (E, 80, 8)).copy()).to(dev), asks, bids, trades)
     rng = np.random.default_rng(3)
+    # the full book: 60 more orders per side, behind the 40 levels of the base book
+    fill = np.zeros((120, 8), np.int32)
+    for j in range(60):
+        fill[2 * j] = (1, 1, 1000, 940 - j, 201 + j, 3, 34200, 100 + j)
+        fill[2 * j + 1] = (1, -1, 1000, 1060 + j, 301 + j, 3, 34200, 100 + j)
+    fa, fb, ft = asks.clone(), bids.clone(), trades.clone()
+    book_process_(w, torch.from_numpy(np.broadcast_to(fill, (E, 120, 8)).copy()).to(dev), fa, fb, ft)
     for kind in ["noop"] + KINDS:
         msgs = torch.from_numpy(np.broadcast_to(stream(kind, rng), (E, N, 8)).copy()).to(dev)
-        a, b, t = asks.clone(), bids.clone(), trades.clone()
+        a, b, t = (fa.clone(), fb.clone(), ft.clone()) if kind in FULL else (asks.clone(), bids.clone(), trades.clone())
         ba = torch.empty((E, N, 2), dtype=torch.int32, device=dev)
         bb = torch.empty_like(ba)
         book_process_(w, msgs, a, b, t, ba, bb)
