@@ -299,10 +299,21 @@ DEV int ffs64(lmask m) { return m ? (int)__builtin_ctzll(m) : -1; }
 extern "C" __device__ i32 __hftlob_writelane(i32 val, i32 lane, i32 old) __asm("llvm.amdgcn.writelane.i32");
 DEV i32 wlane(i32 old, i32 val, int l) { return __hftlob_writelane(val, l, old); }
 
-// Lanes of one wave exchange data through LDS without a barrier (a wave's LDS
-// operations complete in order); this only stops the compiler from moving a
-// load across a store another lane made.
+// Lanes of one wave exchange data through LDS without an s_barrier: every env workgroup is exactly
+// one wave (the launch code's blocks of ENV_BLOCK = 64 threads, checked by one_wave() at each env
+// kernel's entry), and a wave's LDS operations complete in issue order.  lds_order() keeps the
+// compiler from moving an LDS access across a slot write of the message handlers (hot path);
+// wave_sync() adds the wave-level scheduling barrier at the exchanges between phases (agent rows,
+// _filter_messages, the shuffle, the no-op filter, the key batch).
+#define ENV_BLOCK 64
 DEV void lds_order() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+DEV void wave_sync() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+}
+DEV void one_wave() {  // the one-wave-per-workgroup assumption above
+    if (blockDim.x != ENV_BLOCK) __builtin_trap();
+}
 
 enum { FP = 0, FQ, FOID, FTID, FTS, FTNS };  // order-side fields (JaxOrderBookArrays.py:21-28)
 
@@ -1253,7 +1264,7 @@ template <bool RC, int S> DEV lmask chunk_noops(Book<S>& B, const int4& x, const
     i32* f = B.filt;
     if (!B.filt_ok) {  // the book's ids and init-id rows' (price, side), as they are now
         f[l] = 0;
-        lds_order();
+        wave_sync();
         const int R = B.c.nO;
 #pragma unroll
         for (int sd = 0; sd < 2; ++sd) {
@@ -1272,7 +1283,7 @@ template <bool RC, int S> DEV lmask chunk_noops(Book<S>& B, const int4& x, const
     // brk message the filter stays a superset of the book's ids and init rows for the next chunk
     filt_set(f, hash_id(oid), in & add);
     B.filt_ok = brk == 0ull;
-    lds_order();
+    wave_sync();
     const bool ask = kind == H_CNL_ASK;
     const bool hit = (filt_get(f, hash_id(oid)) | filt_get(f, hash_px(price, ask))) != 0u;
     const int room_a = side_room(B, B.a), room_b = side_room(B, B.b);
@@ -1360,6 +1371,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
                                                      i32* __restrict__ asks, i32* __restrict__ bids,
                                                      i32* __restrict__ trades, i32* __restrict__ best_asks,
                                                      i32* __restrict__ best_bids) {
+    one_wave();
     extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
@@ -1708,6 +1720,7 @@ template <int S>
 __global__ __launch_bounds__(64) void k_env_reset(hftlob_env_cfg c, int n_env, const u32* __restrict__ keys,
                                                   const i32* __restrict__ init_states, i32* __restrict__ state,
                                                   float* __restrict__ obs) {
+    one_wave();
     const int e = blockIdx.x;
     if (e >= n_env) return;
     Valid<S> VS, VT;
@@ -1765,7 +1778,7 @@ DEV void cancel_rows(const Side<S>& s, int R, const Valid<S>& V, i32 agent, int 
 // `scratch`: 16 words of LDS.
 template <int n>
 DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
-    lds_order();  // (one-wave workgroups: the rows written above are read back in order, no barrier)
+    wave_sync();  // (one-wave workgroups: the rows written above are read back in order, no barrier)
     const int l = lane_id();
     const bool is_a = l < n, is_c = (l >= 8) & (l < 8 + n);
     const int row = is_a ? arow + l : (is_c ? crow + l - 8 : arow);
@@ -1785,9 +1798,9 @@ DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
     const int cnt = (int)__builtin_amdgcn_mbcnt_hi((u32)(below >> 32), __builtin_amdgcn_mbcnt_lo((u32)below, 0u));
     const int rank = matched ? cnt : (is_a ? na : nc) + cnt;
     if (l < 16) scratch[l] = 0;  // av[k] = scratch[k], cv[k] = scratch[8 + k]
-    lds_order();
+    wave_sync();
     if ((is_a | is_c) & matched) scratch[(is_c ? 8 : 0) + rank] = q;
-    lds_order();
+    wave_sync();
     const i32 av = scratch[rank & 7], cv = scratch[8 + (rank & 7)];
     const i32 nq = wsub(q, cv >= av ? av : 0);
     if (is_a & (nq == 0)) {
@@ -1796,7 +1809,7 @@ DEV void filter_rows(i32* lds_rows, int arow, int crow, i32* scratch) {
     } else if (is_a | is_c) {
         lds_rows[row * 8 + 2] = nq;
     }
-    lds_order();
+    wave_sync();
 }
 
 // MM _getActionMsgs_fixedQuant — mm_env.py:970-1118
@@ -2667,7 +2680,7 @@ DEV void step_keys_batch(const hftlob_env_cfg& c, int n_env, int e, Key& mk, int
     i32 w = ll == 0 ? (i32)key.a : (ll == 1 ? (i32)key.b : ((ll & 1) ? l1b : l1a));
     w = ll >= 6 + c.n_agents ? sh : (ll >= 6 ? ac : w);
     if ((j < nb) & (ll < KW)) kb[j * KW + ll] = w;
-    lds_order();
+    wave_sync();
 }
 // step j's keys from the batch row (as step_keys would derive them)
 DEV StepKeys load_keys(const hftlob_env_cfg& c, const i32* row) {
@@ -2986,7 +2999,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             }
         }
     }
-    lds_order();
+    wave_sync();
     SUBSTAMP(t_rows);
     // order ids (counter - j) and the action-row permutation (lane j = action row j)
     {
@@ -3007,12 +3020,12 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
             }
             dest = rank;
         }
-        lds_order();
+        wave_sync();
         if (act_lane) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) rows[(C + dest) * 8 + k] = f[k];
         }
-        lds_order();
+        wave_sync();
     }
 
     STAMP(t_agents);
@@ -3051,7 +3064,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
                 nx = reinterpret_cast<const int4*>(rows + (row + 64) * 8)[0];  // operations run in order)
                 ny = reinterpret_cast<const int4*>(rows + (row + 64) * 8)[1];
             }
-            lds_order();
+            wave_sync();
             trades_fill(B.tr, B.vt, -1);
         }
         decode_msgs(B.c, x, y);
@@ -3269,6 +3282,7 @@ __global__ __launch_bounds__(64) void k_env_step(hftlob_env_cfg c, int n_env, in
                                                  u32* __restrict__ master_out, i32* __restrict__ actions_io,
                                                  const i32* __restrict__ msg_data, const i32* __restrict__ init_states,
                                                  i32* __restrict__ state, hftlob_step_out out) {
+    one_wave();
     extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
@@ -3348,6 +3362,7 @@ __global__ __launch_bounds__(64, 4) void k_env_rollout(hftlob_env_cfg c, int n_e
                                                     const i32* __restrict__ msg_data,
                                                     const i32* __restrict__ init_states, i32* __restrict__ state,
                                                     hftlob_step_out out) {
+    one_wave();
     extern __shared__ __attribute__((aligned(16))) i32 lds[];
     const int e = blockIdx.x;
     if (e >= n_env) return;
@@ -3580,7 +3595,7 @@ int hftlob_book_process(const hftlob_lob_cfg* cfg, int n_env, int n_msg, const u
     if (rc_ && !keys) return fail(HFTLOB_ENULL, "keys required for cancel_mode 2/3");
     const int S = slot_sets(cfg->n_orders > cfg->n_trades ? cfg->n_orders : cfg->n_trades);
     hipStream_t st = (hipStream_t)stream;
-    dim3 g(n_env), b(64);
+    dim3 g(n_env), b(ENV_BLOCK);
     const size_t shm = 4 * ((size_t)12 * cfg->n_orders + 8 * cfg->n_trades + 64 * 4);
 #define LAUNCH_BOOK(SS, RC) hipLaunchKernelGGL((k_book_process<SS, RC>), g, b, shm, st, *cfg, n_env, n_msg, keys, msgs, \
                                                asks, bids, trades, best_asks, best_bids)
@@ -3673,7 +3688,7 @@ int hftlob_env_reset(const hftlob_env_cfg* cfg, int n_env, const uint32_t* keys,
     float* obs = out ? out->obs : nullptr;
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
-    dim3 g(n_env), b(64);
+    dim3 g(n_env), b(ENV_BLOCK);
     const hftlob_env_cfg kc = kernel_cfg(cfg);
     if (S == 1) hipLaunchKernelGGL(k_env_reset<1>, g, b, 0, st, kc, n_env, keys, init_states, state, obs);
     else if (S == 2) hipLaunchKernelGGL(k_env_reset<2>, g, b, 0, st, kc, n_env, keys, init_states, state, obs);
@@ -3707,7 +3722,7 @@ static int env_step_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, int
     if (!out->obs || !out->rewards || !out->done_all || !out->dones) return fail(HFTLOB_ENULL, "null output");
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
-    dim3 g(n_env), b(64);
+    dim3 g(n_env), b(ENV_BLOCK);
     const size_t shm = env_shm(cfg);
     const hftlob_env_cfg kc = kernel_cfg(cfg);
 #define LAUNCH_STEP(SS, NF, RC) hipLaunchKernelGGL((k_env_step<SS, NF, RC>), g, b, shm, st, kc, n_env, key_e0, key_n, keys, \
@@ -3734,7 +3749,7 @@ static int env_rollout_launch(const hftlob_env_cfg* cfg, int n_env, int key_e0, 
                               const int32_t* init_states, int32_t* state, const hftlob_step_out* out, void* stream) {
     const int S = slot_sets(cfg->lob.n_orders > cfg->lob.n_trades ? cfg->lob.n_orders : cfg->lob.n_trades);
     hipStream_t st = (hipStream_t)stream;
-    dim3 g(n_env), b(64);
+    dim3 g(n_env), b(ENV_BLOCK);
     const size_t shm = env_shm(cfg);
     const hftlob_env_cfg kc = kernel_cfg(cfg);
 #define LAUNCH_ROLL(SS, NF, RC) hipLaunchKernelGGL((k_env_rollout<SS, NF, RC>), g, b, shm, st, kc, n_env, key_e0, key_n, \
