@@ -421,23 +421,24 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 //   NEG1   some row with p != -1 holds a -1 in another field (then "first row
 //          holding ANY -1" needs the full test, else p == -1 suffices)
 //   PM1    some row with p == -1 holds a field != -1 (an order priced -1)
-//   FAST   both sides CLEAN, neither NEG1 nor PM1 (the handlers' common variant): then a
-//          row holds a -1 <=> its price is -1 <=> it is all -1, so the free slots are the
-//          p == -1 slots of the register price column
+//   SLOW   not FAST.  FAST: both sides CLEAN, neither NEG1 nor PM1 (the handlers' common
+//          variant): then a row holds a -1 <=> its price is -1 <=> it is all -1, so the free
+//          slots are the p == -1 slots of the register price column.  Kept inverted so the
+//          one test after a FAST message, "a side is stale or the book is no longer FAST", is
+//          one s_and with the STALE bits (run_chunk)
 // (bit 0 is left unused: a branch on a bit-0 test compiles to s_bitcmp1 + a 64-bit lane mask
-// + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc.  F_FAST,
-// tested once per message, is the sign bit: (i32)fl < 0 is one s_cmp_lt_i32)
+// + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc)
 enum : u32 { F_STALE_A = 2, F_STALE_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64,
-             F_PM1_A = 256, F_PM1_B = 512, F_FAST = 0x80000000u };
+             F_PM1_A = 256, F_PM1_B = 512, F_SLOW = 0x40000000u };
 template <bool ASKS> struct SideBits {
     static constexpr u32 STALE = ASKS ? F_STALE_A : F_STALE_B;
     static constexpr u32 CLEAN = ASKS ? F_CLEAN_A : F_CLEAN_B;
     static constexpr u32 NEG1 = ASKS ? F_NEG1_A : F_NEG1_B;
     static constexpr u32 PM1 = ASKS ? F_PM1_A : F_PM1_B;
 };
-DEV u32 fast_bit(u32 fl) {
+DEV u32 slow_bit(u32 fl) {
     return (fl & (F_CLEAN_A | F_CLEAN_B | F_NEG1_A | F_NEG1_B | F_PM1_A | F_PM1_B)) == (F_CLEAN_A | F_CLEAN_B)
-               ? F_FAST : 0u;
+               ? 0u : F_SLOW;
 }
 
 // A side's rows in registers between the global load and the LDS commit, so
@@ -540,7 +541,7 @@ template <bool ASKS, int S> DEV void rzn(Side<S>& s, u32& fl, int R, const Valid
     for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
     clear_masked(s, R, m);
     fl = fl | SideBits<ASKS>::CLEAN | SideBits<ASKS>::STALE;
-    fl = (fl & ~F_FAST) | fast_bit(fl);
+    fl = (fl & ~F_SLOW) | slow_bit(fl);
 }
 
 // get_best_bid: max raw price (empty side -> -1); volume at it — :943-951,906-917
@@ -663,7 +664,7 @@ DEV void trade_put(Trades& T, int e, i32 f0, i32 f1, i32 f2, i32 f3, i32 f4, i32
 // ------------------------------------------------------ message handlers
 // G (general) = false instantiates the handlers for the common case where
 // both sides are clean and neg1-free (flags that only add_order can change):
-// the kernels run that variant while F_FAST is set.
+// the kernels run that variant while F_SLOW is clear.
 template <int S>
 struct Book {
     Side<S> a, b;
@@ -840,12 +841,14 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
 // beats the side's best, so "best does not cross" ends the loop exactly; only
 // a crossing best pays for the 3-reduction top-of-book.
 // a crossing trip loads every column it needs at once (one LDS round trip)
-template <bool BID, bool G, int S> DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
+// POS: qtm > 0 is known (the common FAST adds, decode_msgs)
+template <bool BID, bool G, int S, bool POS = false>
+DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) {
     const int R = B.c.nO;
     // the common case first, as straight-line scalar code: nothing to match, or a best that
     // does not cross (the loop's own first test, with an empty ask side standing for maxint)
     // (fresh: the RARE / common handler copies each keep their own test, not one shared lane mask)
-    if (fresh(qtm) <= 0) return qtm;
+    if (!POS && fresh(qtm) <= 0) return qtm;
     // (no stale side here: run_chunk refreshes both sides after every message)
     {
         const i32 bp = s.best_p;
@@ -908,7 +911,7 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         const bool was_empty = !no_slot(free);
         if (nq > 0) {
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
-            if (m.h & (H_NEG1 | H_PM1)) B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
+            if (m.h & (H_NEG1 | H_PM1)) B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
             if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
             else { B.fl |= STALE; s.top = -1; }
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
@@ -992,7 +995,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         // rare: kept as a branch (the empty asm stops if-conversion into ~10 scalar selects per add)
         asm volatile("");
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
-        B.fl = (B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u)) & ~F_FAST;
+        B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
     }
     note_add<BID, S, false>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
 }
@@ -1001,7 +1004,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
 // tests are compiled out of the common FAST add
 template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
-    const i32 rem = match_against<false, G>(B, B.a, m.qty, m.price, m);
+    const i32 rem = match_against<false, G, S, !RARE && !G>(B, B.a, m.qty, m.price, m);
     if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = B.c.maxint;  // MKT: set after matching (sic)
     lmask free[S];
     free_slots(B, B.b, free);
@@ -1018,7 +1021,7 @@ template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
 template <bool G, bool RARE, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = 0;
-    const i32 rem = match_against<true, G>(B, B.b, m.qty, m.price, m);
+    const i32 rem = match_against<true, G, S, !RARE && !G>(B, B.b, m.qty, m.price, m);
     lmask free[S];
     free_slots(B, B.a, free);
     if (!no_slot(free)) {
@@ -1180,11 +1183,7 @@ DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5,
         else ask_lim<G, true>(B, m);
     }
 }
-template <bool RC, int S>
-DEV void process_msg(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
-    if ((i32)B.fl < 0) process_msg_<false, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);  // F_FAST
-    else process_msg_<true, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
-}
+
 // forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
 DEV i32 ffill(i32 v, i32 carry) {
     const int l = lane_id();
@@ -1249,7 +1248,7 @@ template <bool RC, int S> DEV lmask chunk_noops(Book<S>& B, const int4& x, const
     const i32 kind = x.x & H_KIND, qty = x.z, price = x.w, oid = y.x;
     const bool in = l < cnt;
     const lmask nop = bal(in & (kind == H_NOP));
-    if ((i32)B.fl >= 0) {  // not FAST
+    if (B.fl & F_SLOW) {  // not FAST
         B.filt_ok = false;
         return nop;
     }
@@ -1322,7 +1321,8 @@ DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, 
         do {
             asm volatile("s_bitset0_b64 %0, %1" : "+s"(todo) : "s"(k));
             if (RC) B.mi = base + (int)k;
-            process_msg<RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
+            if (!(B.fl & F_SLOW)) process_msg_<false, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
+            else process_msg_<true, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
             refresh_best(B);
             const u32 kn = ff1(todo);  // (-1 once todo is empty: v_readlane takes the lane's low 6 bits)
             h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
@@ -1384,7 +1384,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     i32* gb = bids + (size_t)e * R * 6;
     i32* gt = trades + (size_t)e * B.c.nT * 8;
     B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs) | F_STALE_A | F_STALE_B;
-    B.fl |= fast_bit(B.fl);
+    B.fl |= slow_bit(B.fl);
     load_trades(B.tr, gt, B.vt);
     {  // the loaded log's free-row prefix (see Book::ntr)
         lmask fr[S], bad = 0;
@@ -2867,7 +2867,7 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         B.fl = fl_carry | F_STALE_A | F_STALE_B;
     } else {
         B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs) | F_STALE_A | F_STALE_B;
-        B.fl |= fast_bit(B.fl);
+        B.fl |= slow_bit(B.fl);
     }
     SUBSTAMP(t_load);
 
