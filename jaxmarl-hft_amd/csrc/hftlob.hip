@@ -402,7 +402,18 @@ struct Side {
     // row (or any bulk clear) drops it, an add at a better price or an earlier time at top_p
     // replaces it (see top_new / top_eq), so a crossing message usually skips the top-of-book scan
     i32 top, top_p, top_ts, top_tns;
+    // the chunk's best-quote record of this side (run_chunk): lane k holds (best_p, best_q) after
+    // message k if the message set or recomputed them (lane k of rm), else the lanes are filled
+    // from the last recording lane before them when the chunk ends
+    i32 rp, rq;
+    lmask rm;
 };
+// a message (its lane k of the chunk) set or recomputed the side's best quote: record it
+template <int S> DEV void side_rec(Side<S>& s, u32 k) {
+    s.rp = wlane(s.rp, s.best_p, (int)k);
+    s.rq = wlane(s.rq, s.best_q, (int)k);
+    asm volatile("s_bitset1_b64 %0, %1" : "+s"(s.rm) : "s"(k));
+}
 
 // slot e of a lane-strided register column <- v (lane e & 63 of register e >> 6): one
 // compare and one select per register set, no scalar work
@@ -570,13 +581,16 @@ DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i3
     bp = pa;
     bq = wave_sum(v);
 }
-// recompute a side's cached best quote (clears its STALE bit)
-template <bool ASKS, int S> DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint) {
+// recompute a side's cached best quote (clears its STALE bit); REC: inside message k's
+// processing, which then records the quote
+template <bool ASKS, bool REC, int S>
+DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint, u32 k) {
     i32 q[S];
     ldcol(s.t, R, FQ, q);
     if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q);
     else best_bid_pq(s.pc, q, V, s.best_p, s.best_q);
     fl &= ~SideBits<ASKS>::STALE;
+    if (REC) side_rec(s, k);
 }
 
 // _get_top_bid_order_idx / _get_top_ask_order_idx — :241-268 (exact formulas);
@@ -692,6 +706,7 @@ enum { H_ASK = 0, H_BID = 1, H_CNL_ASK = 2, H_CNL_BID = 3, H_NOP = 4, H_KIND = 7
        H_PM1 = 32, H_MKT = 64, H_RARE = 128 };
 struct Msg {
     i32 h, side, price, qty, oid, tid, t, tns;  // h: handler code and H_* flags (decode_msgs)
+    u32 k;                                      // its lane in the chunk (the best-quote record's)
 };
 
 // Incremental best-quote bookkeeping.  Every update below is exact for a clean
@@ -724,7 +739,7 @@ template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) 
 // stale side, run_chunk refreshes both after each one, and an add without eviction changes only
 // the other side before it gets here)
 template <bool BID, int S, bool STALE_OK = true>
-DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint) {
+DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint, u32 k) {
     // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
     // common case, an order behind the best (one compare each); per side the cases are those of
     // get_best_* with -1 (and, for asks, maxint) standing for "no price".
@@ -736,31 +751,34 @@ DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i3
             if (bp == -1) fl |= STALE;        // np < -1 on an empty side
         } else if (np > bp) {
             s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
+            side_rec(s, k);
             top_new(s, e, np, t, tns, maxint);
         } else if (bp == -1) {
             fl |= STALE;                      // np == -1 on an empty side
         } else {
             s.best_q = wadd(s.best_q, nq);
+            side_rec(s, k);
             top_eq(s, e, t, tns, maxint);
         }
     } else {
         if (np > bp) {
             if (bp == -1) {                 // empty side
                 if (np == maxint) fl |= STALE;
-                else { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
+                else { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
             }
         } else if (np < bp) {
-            if (np != -1) { s.best_p = np; s.best_q = nq; top_new(s, e, np, t, tns, maxint); }
+            if (np != -1) { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
         } else if (np == -1) {
             fl |= STALE;
         } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
+            side_rec(s, k);
             top_eq(s, e, t, tns, maxint);
         }
     }
 }
 // a row at price op lost dq of its quantity (possibly all of it)
-template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i32 dq) {
+template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i32 dq, u32 k) {
     constexpr u32 STALE = SideBits<ASKS>::STALE;
     if (fl & STALE) return;
     if (op == s.best_p) {
@@ -768,6 +786,7 @@ template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i3
             fl |= STALE;
         } else {
             s.best_q = wsub(s.best_q, dq);
+            side_rec(s, k);
             if (s.best_q <= 0) fl |= STALE;  // level exhausted (or odd data): rescan
         }
     } else {
@@ -829,7 +848,7 @@ DEV i32 match_order(Book<S>& B, Side<S>& s, int top, i32 qtm, const Msg& m, i32 
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (newq <= 0) side_clr(s, R, top);
         else stu(s.t, s.scr, R, FQ, top, newq);
-        note_reduce<ASKS>(s, B.fl, pt, wsub(qt, newq));
+        note_reduce<ASKS>(s, B.fl, pt, wsub(qt, newq), m.k);
     } else {
         stu(s.t, s.scr, R, FQ, top, newq);
         rzn<ASKS>(s, B.fl, R, B.vs);
@@ -856,7 +875,7 @@ DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) 
         if (__builtin_expect(BID ? mp0 < price : mp0 > price, 1)) return qtm;
     }
     while (qtm > 0) {
-        if (B.fl & SideBits<!BID>::STALE) rescan<!BID>(s, B.fl, R, B.vs, B.c.maxint);
+        if (B.fl & SideBits<!BID>::STALE) rescan<!BID, true>(s, B.fl, R, B.vs, B.c.maxint, m.k);
         // the side's best; an empty ask side (-1) counts as maxint (_get_top_ask_order_idx).
         // BID: `s` is the bid side (an incoming sell crosses when best bid >= price)
         i32 mp = s.best_p;
@@ -912,7 +931,7 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         if (nq > 0) {
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
             if (m.h & (H_NEG1 | H_PM1)) B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
-            if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
+            if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint, m.k);
             else { B.fl |= STALE; s.top = -1; }
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
             side_clr(s, R, e);
@@ -948,7 +967,7 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
         if (m.h & H_NEG1) B.fl |= NEG1;
         if (m.h & H_PM1) B.fl |= PM1;
-        if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint);
+        if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint, m.k);
         else { B.fl |= STALE; s.top = -1; }
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         side_clr(s, R, e);
@@ -997,7 +1016,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
     }
-    note_add<BID, S, false>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint);
+    note_add<BID, S, false>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint, m.k);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
@@ -1133,7 +1152,7 @@ template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
         if (nq <= 0) side_clr(s, R, idx);
         else stu(s.t, s.scr, R, FQ, idx, nq);
-        note_reduce<ASKS>(s, B.fl, op, wsub(oq, nq > 0 ? nq : 0));
+        note_reduce<ASKS>(s, B.fl, op, wsub(oq, nq > 0 ? nq : 0), m.k);
     } else {
         stu(s.t, s.scr, R, FQ, idx, nq);
         rzn<ASKS>(s, B.fl, R, B.vs);
@@ -1169,9 +1188,10 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     x.y = sd;
 }
 template <bool G, bool RC, int S>
-DEV void process_msg_(Book<S>& B, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+DEV void process_msg_(Book<S>& B, u32 k, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
     m.h = h; m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
+    m.k = k;
     const i32 kind = h & H_KIND;
     if (kind == H_CNL_ASK) cancel<G, true, RC>(B, B.a, m);
     else if (kind == H_CNL_BID) cancel<G, false, RC>(B, B.b, m);
@@ -1192,10 +1212,11 @@ DEV i32 ffill(i32 v, i32 carry) {
     const i32 got = __builtin_amdgcn_ds_bpermute(src << 2, v);
     return src < 0 ? carry : got;
 }
-template <int S> DEV void refresh_best(Book<S>& B) {
+// REC: after message k (which records the recomputed quotes), not at a chunk's start
+template <bool REC = true, int S> DEV void refresh_best(Book<S>& B, u32 k = 0) {
     if (B.fl & (F_STALE_A | F_STALE_B)) {
-        if (B.fl & F_STALE_A) rescan<true>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint);
-        if (B.fl & F_STALE_B) rescan<false>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint);
+        if (B.fl & F_STALE_A) rescan<true, REC>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint, k);
+        if (B.fl & F_STALE_B) rescan<false, REC>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint, k);
     }
 }
 
@@ -1310,8 +1331,13 @@ DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, 
 #ifdef HFTLOB_KO_LOOP  // timing knockout builds only (wrong results): no message reaches the book
     todo = 0;
 #endif
-    refresh_best(B);
+    refresh_best<false>(B);
     const i32 cpa = B.a.best_p, cqa = B.a.best_q, cpb = B.b.best_p, cqb = B.b.best_q;  // before the chunk
+    // the best-quote record: a message that sets or recomputes a side's quote writes it into its
+    // lane of that side's record (side_rec, at the assignment); the other lanes take the last
+    // record before them below (the book, hence that quote, is unchanged since)
+    B.a.rm = B.b.rm = 0ull;
+    B.a.rp = B.a.rq = B.b.rp = B.b.rq = 0;
     if (todo) {
         // message k's fields are read (v_readlane) at the end of the message before it, so their
         // latency overlaps the best-quote record and the loop test instead of stalling the dispatch
@@ -1321,28 +1347,26 @@ DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, 
         do {
             asm volatile("s_bitset0_b64 %0, %1" : "+s"(todo) : "s"(k));
             if (RC) B.mi = base + (int)k;
-            if (!(B.fl & F_SLOW)) process_msg_<false, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
-            else process_msg_<true, RC>(B, h, d1, d2, d3, d4, d5, d6, d7);
-            refresh_best(B);
+            if (!(B.fl & F_SLOW)) process_msg_<false, RC>(B, k, h, d1, d2, d3, d4, d5, d6, d7);
+            else process_msg_<true, RC>(B, k, h, d1, d2, d3, d4, d5, d6, d7);
+            refresh_best(B, k);
             const u32 kn = ff1(todo);  // (-1 once todo is empty: v_readlane takes the lane's low 6 bits)
             h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
             d4 = rdl(y.x, kn); d5 = rdl(y.y, kn); d6 = rdl(y.z, kn); d7 = rdl(y.w, kn);
-            rpa = wlane(rpa, B.a.best_p, k); rqa = wlane(rqa, B.a.best_q, k);
-            rpb = wlane(rpb, B.b.best_p, k); rqb = wlane(rqb, B.b.best_q, k);
             k = kn;
         } while (todo);
     }
-    if (skip) {  // the skipped lanes take the record of the last message run before them
+    {  // every lane takes its side's last record at or before it (or the chunk's starting quote)
         const int l = lane_id();
-        const lmask m = live & ~skip & (~0ull >> (63 - l));
-        const int src = m ? 63 - __builtin_clzll(m) : -1;
-        const i32 gpa = __builtin_amdgcn_ds_bpermute(src << 2, rpa), gqa = __builtin_amdgcn_ds_bpermute(src << 2, rqa);
-        const i32 gpb = __builtin_amdgcn_ds_bpermute(src << 2, rpb), gqb = __builtin_amdgcn_ds_bpermute(src << 2, rqb);
-        const bool own = (skip >> l) & 1ull;
-        rpa = own ? (src < 0 ? cpa : gpa) : rpa;
-        rqa = own ? (src < 0 ? cqa : gqa) : rqa;
-        rpb = own ? (src < 0 ? cpb : gpb) : rpb;
-        rqb = own ? (src < 0 ? cqb : gqb) : rqb;
+        const lmask below = ~0ull >> (63 - l);
+        const lmask ma = B.a.rm & below, mb = B.b.rm & below;
+        const int sa = ma ? 63 - __builtin_clzll(ma) : -1, sb = mb ? 63 - __builtin_clzll(mb) : -1;
+        const i32 gpa = __builtin_amdgcn_ds_bpermute(sa << 2, B.a.rp), gqa = __builtin_amdgcn_ds_bpermute(sa << 2, B.a.rq);
+        const i32 gpb = __builtin_amdgcn_ds_bpermute(sb << 2, B.b.rp), gqb = __builtin_amdgcn_ds_bpermute(sb << 2, B.b.rq);
+        rpa = sa < 0 ? cpa : gpa;
+        rqa = sa < 0 ? cqa : gqa;
+        rpb = sb < 0 ? cpb : gpb;
+        rqb = sb < 0 ? cqb : gqb;
     }
 }
 
