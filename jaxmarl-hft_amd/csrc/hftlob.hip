@@ -439,9 +439,20 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 // (bit 0 is left unused: a branch on a bit-0 test compiles to s_bitcmp1 + a 64-bit lane mask
 // + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc)
 enum : u32 { F_STALE_A = 2, F_STALE_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64,
-             F_PM1_A = 256, F_PM1_B = 512, F_SLOW = 0x80000000u };
+             F_PM1_A = 256, F_PM1_B = 512, F_STALE_ANY = 0x40000000u, F_SLOW = 0x80000000u };
+#ifdef HFTLOB_X_ANY
+constexpr u32 STALE_ANY = F_STALE_ANY;  // set with either side's STALE bit: one bit test after each message
+#else
+constexpr u32 STALE_ANY = 0;
+#endif
+#ifdef HFTLOB_X_NN
+constexpr bool NNADD = true;
+#else
+constexpr bool NNADD = false;
+#endif
 template <bool ASKS> struct SideBits {
     static constexpr u32 STALE = ASKS ? F_STALE_A : F_STALE_B;
+    static constexpr u32 MARK = STALE | STALE_ANY;  // (sets STALE)
     static constexpr u32 CLEAN = ASKS ? F_CLEAN_A : F_CLEAN_B;
     static constexpr u32 NEG1 = ASKS ? F_NEG1_A : F_NEG1_B;
     static constexpr u32 PM1 = ASKS ? F_PM1_A : F_PM1_B;
@@ -550,7 +561,7 @@ template <bool ASKS, int S> DEV void rzn(Side<S>& s, u32& fl, int R, const Valid
 #pragma unroll
     for (int r = 0; r < S; ++r) m[r] = V.m[r] & bal(q[r] <= 0);
     clear_masked(s, R, m);
-    fl = fl | SideBits<ASKS>::CLEAN | SideBits<ASKS>::STALE;
+    fl = fl | SideBits<ASKS>::CLEAN | SideBits<ASKS>::MARK;
     fl = (fl & ~F_SLOW) | slow_bit(fl);
 }
 
@@ -737,25 +748,24 @@ template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) 
 // STALE_OK = false: the caller knows the side is not stale (add_free: no message starts with a
 // stale side, run_chunk refreshes both after each one, and an add without eviction changes only
 // the other side before it gets here)
-// (returns whether the side is stale afterwards: add_free's caller skips the refresh otherwise)
-template <bool BID, int S, bool STALE_OK = true>
-DEV bool note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint, u32 k) {
+// NN: np >= 0 is known (the common adds: decode_msgs marks negative prices RARE)
+template <bool BID, int S, bool STALE_OK = true, bool NN = false>
+DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint, u32 k) {
     // an all -1 row (slot e) now holds (np, nq > 0, time t / tns).  Branches ordered for the
     // common case, an order behind the best (one compare each); per side the cases are those of
     // get_best_* with -1 (and, for asks, maxint) standing for "no price".
-    constexpr u32 STALE = SideBits<!BID>::STALE;
-    if (STALE_OK && (fl & STALE)) { s.top = -1; return true; }
+    constexpr u32 STALE = SideBits<!BID>::STALE, MARK = SideBits<!BID>::MARK;
+    if (STALE_OK && (fl & STALE)) { s.top = -1; return; }
     const i32 bp = s.best_p;
     if (BID) {
         if (np < bp) {
-            if (bp == -1) { fl |= STALE; return true; }  // np < -1 on an empty side
+            if (!NN && bp == -1) fl |= MARK;  // np < -1 on an empty side
         } else if (np > bp) {
             s.best_p = np; s.best_q = nq;   // (an empty side: np > -1)
             side_rec(s, k);
             top_new(s, e, np, t, tns, maxint);
-        } else if (bp == -1) {
-            fl |= STALE;                      // np == -1 on an empty side
-            return true;
+        } else if (!NN && bp == -1) {
+            fl |= MARK;                       // np == -1 on an empty side
         } else {
             s.best_q = wadd(s.best_q, nq);
             side_rec(s, k);
@@ -764,41 +774,39 @@ DEV bool note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i3
     } else {
         if (np > bp) {
             if (bp == -1) {                 // empty side
-                if (np == maxint) { fl |= STALE; return true; }
-                s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint);
+                if (np == maxint) fl |= MARK;
+                else { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
             }
         } else if (np < bp) {
-            if (np != -1) { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
-        } else if (np == -1) {
-            fl |= STALE;
-            return true;
+            if (NN || np != -1) { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
+        } else if (!NN && np == -1) {
+            fl |= MARK;
         } else if (np != maxint) {
             s.best_q = wadd(s.best_q, nq);
             side_rec(s, k);
             top_eq(s, e, t, tns, maxint);
         }
     }
-    return false;
 }
 // a row at price op lost dq of its quantity (possibly all of it)
 template <bool ASKS, int S> DEV void note_reduce(Side<S>& s, u32& fl, i32 op, i32 dq, u32 k) {
-    constexpr u32 STALE = SideBits<ASKS>::STALE;
+    constexpr u32 STALE = SideBits<ASKS>::STALE, MARK = SideBits<ASKS>::MARK;
     if (fl & STALE) return;
     if (op == s.best_p) {
         if (op == -1) {
-            fl |= STALE;
+            fl |= MARK;
         } else {
             s.best_q = wsub(s.best_q, dq);
             side_rec(s, k);
-            if (s.best_q <= 0) fl |= STALE;  // level exhausted (or odd data): rescan
+            if (s.best_q <= 0) fl |= MARK;  // level exhausted (or odd data): rescan
         }
     } else {
         // a row behind the best: the quote stands unless a -1 price is involved (scalar selects;
         // as one branch on "op == -1 || best == -1" the compiler builds 64-bit lane masks)
         asm volatile("");
         u32 f = fl;
-        f = fresh(op) == -1 ? f | STALE : f;
-        f = fresh(s.best_p) == -1 ? f | STALE : f;
+        f = fresh(op) == -1 ? f | MARK : f;
+        f = fresh(s.best_p) == -1 ? f | MARK : f;
         fl = f;
     }
 }
@@ -925,7 +933,7 @@ DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) 
 template <bool BID, bool G, int S>
 DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
-    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, STALE = SideBits<!BID>::STALE,
+    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, STALE = SideBits<!BID>::MARK,
                   PM1 = SideBits<!BID>::PM1;
     const i32 nq = imax_(0, qty);
     if (!G) {  // FAST: "any -1" <=> p == -1 <=> an all -1 row; no free slot -> the last slot, which holds an order
@@ -999,7 +1007,7 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
     // only the worst level goes: the best quote and the top of book survive unless the side holds
     // one price level (worst == best; an ask side whose prices are all maxint has best -1)
     s.top = worst != s.top_p ? top : -1;
-    if ((worst == s.best_p) | (s.best_p == -1)) B.fl |= SideBits<!BID>::STALE;
+    if ((worst == s.best_p) | (s.best_p == -1)) B.fl |= SideBits<!BID>::MARK;
     free_slots(B, s, free);
 }
 // The common add: FAST book, a free (all -1) slot exists, no eviction: the order goes to the
@@ -1007,9 +1015,9 @@ template <bool BID, int S> DEV void evict_if_full(Book<S>& B, Side<S>& s, lmask 
 // -1 fields), so they stay behind a branch.
 // POS: qty > 0 is known (the common add that does not cross)
 template <bool BID, bool RARE, int S, bool POS = false>
-DEV bool add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
+DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
-    if (!POS && qty <= 0) return false;  // imax(0, qty) == 0: the new row is removed at once and the slot was empty
+    if (!POS && qty <= 0) return;  // imax(0, qty) == 0: the new row is removed at once and the slot was empty
     u32 e = ff1(free[0]);
 #pragma unroll
     for (int r = 1; r < S; ++r) e = min(e, ff1(free[r]) | (u32)(64 * r));
@@ -1020,13 +1028,12 @@ DEV bool add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
     }
-    return note_add<BID, S, false>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint, m.k);
+    note_add<BID, S, false, NNADD && !RARE>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint, m.k);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
 // tests are compiled out of the common FAST add
-// (returns false where the book's best quotes are known fresh afterwards: run_chunk's refresh test)
-template <bool G, bool RARE, int S> DEV bool bid_lim(Book<S>& B, Msg m) {
+template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     constexpr bool POS = !RARE && !G;
     if (POS) {  // the common add: it does not cross (an empty ask side stands for maxint), so all of it goes in
@@ -1034,10 +1041,13 @@ template <bool G, bool RARE, int S> DEV bool bid_lim(Book<S>& B, Msg m) {
         if (__builtin_expect((bp == -1 ? B.c.maxint : bp) > m.price, 1)) {
             lmask free[S];
             free_slots(B, B.b, free);
-            if (!no_slot(free)) return add_free<true, false, S, true>(B, B.b, m, m.qty, free);
+            if (!no_slot(free)) {
+                add_free<true, false, S, true>(B, B.b, m, m.qty, free);
+                return;
+            }
             if (B.c.check_fill) evict_if_full<true>(B, B.b, free);
             add_order<true, G>(B, B.b, m, m.qty, free);
-            return true;
+            return;
         }
     }
     const i32 rem = match_against<false, G, S, POS>(B, B.a, m.qty, m.price, m);
@@ -1048,24 +1058,26 @@ template <bool G, bool RARE, int S> DEV bool bid_lim(Book<S>& B, Msg m) {
         // FAST: a discarded add is an add of nothing (add_free returns at once for qty <= 0)
         if (!G) add_free<true, RARE>(B, B.b, m, (RARE && (m.h & H_DISCARD)) ? 0 : rem, free);
         else if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
-        return true;
+        return;
     }
     if (B.c.check_fill) evict_if_full<true>(B, B.b, free);
     if (!(m.h & H_DISCARD)) add_order<true, G>(B, B.b, m, rem, free);
-    return true;
 }
 // ask_lim — :446-508
-template <bool G, bool RARE, int S> DEV bool ask_lim(Book<S>& B, Msg m) {
+template <bool G, bool RARE, int S> DEV void ask_lim(Book<S>& B, Msg m) {
     if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     if (RARE && __builtin_expect((m.h & H_MKT) != 0, 0)) m.price = 0;
     constexpr bool POS = !RARE && !G;
     if (POS && __builtin_expect(B.b.best_p < m.price, 1)) {  // the common add: it does not cross
         lmask free[S];
         free_slots(B, B.a, free);
-        if (!no_slot(free)) return add_free<false, false, S, true>(B, B.a, m, m.qty, free);
+        if (!no_slot(free)) {
+            add_free<false, false, S, true>(B, B.a, m, m.qty, free);
+            return;
+        }
         if (B.c.check_fill) evict_if_full<false>(B, B.a, free);
         add_order<false, G>(B, B.a, m, m.qty, free);
-        return true;
+        return;
     }
     const i32 rem = match_against<true, G, S, POS>(B, B.b, m.qty, m.price, m);
     lmask free[S];
@@ -1073,11 +1085,10 @@ template <bool G, bool RARE, int S> DEV bool ask_lim(Book<S>& B, Msg m) {
     if (!no_slot(free)) {
         if (!G) add_free<false, RARE>(B, B.a, m, (RARE && (m.h & H_DISCARD)) ? 0 : rem, free);
         else if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, free);
-        return true;
+        return;
     }
     if (B.c.check_fill) evict_if_full<false>(B, B.a, free);
     if (!(m.h & H_DISCARD)) add_order<false, G>(B, B.a, m, rem, free);
-    return true;
 }
 // get_random_id_match / get_random_large_id_match — :141-164 (cancel_mode 2/3).
 // key = split(key)[0]; chosen = jax.random.choice(key, ids, p=|sign(ids)|),
@@ -1119,11 +1130,11 @@ DEV int random_id_match(const Book<S>& B, Key& k, const i32 (&o)[S], const lmask
     return first_slot(f, -1);
 }
 // cancel_order + get_init_id_match — :93-139 (+ :141-164 when RC)
-template <bool G, bool ASKS, bool RC, int S> DEV bool cancel(Book<S>& B, Side<S>& s, const Msg& m) {
+template <bool G, bool ASKS, bool RC, int S> DEV void cancel(Book<S>& B, Side<S>& s, const Msg& m) {
     // On clean sides (the !G variant) a zero-quantity cancel changes nothing: whichever row it
     // picks keeps q (or, empty, stays all -1) and the best quote is unchanged.  The agents'
     // unused cancel rows (getCancelMsgs' zero rows) are such messages.
-    if (!G && m.qty == 0) return false;
+    if (!G && m.qty == 0) return;
     const int R = B.c.nO;
     i32 o[S], q[S];
     ldcol(s.t, R, FOID, o);
@@ -1174,7 +1185,7 @@ template <bool G, bool ASKS, bool RC, int S> DEV bool cancel(Book<S>& B, Side<S>
     // unit, 8 instructions instead of 3 / 5)
     if (!G && fresh(op & oq) == -1) {
         asm volatile("");
-        if (m.qty >= -1) return false;
+        if (m.qty >= -1) return;
     }
     const i32 nq = wsub(oq, m.qty);
     if (!G || (B.fl & SideBits<ASKS>::CLEAN)) {
@@ -1185,7 +1196,6 @@ template <bool G, bool ASKS, bool RC, int S> DEV bool cancel(Book<S>& B, Side<S>
         stu(s.t, s.scr, R, FQ, idx, nq);
         rzn<ASKS>(s, B.fl, R, B.vs);
     }
-    return true;
 }
 
 // cond_type_side_save_bidask — :687-732: dispatch index
@@ -1213,48 +1223,41 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     if (c.t4 == 2) h |= H_MKT;    // type_4_interpretation MKT: the limit handlers' price overrides
     if (h & (H_DISCARD | H_NEG1 | H_PM1 | H_MKT)) h |= H_RARE;
     if ((h <= H_BID) & (x.z <= 0)) h |= H_RARE;  // an add of no quantity (the common add handlers assume qty > 0)
-#ifdef HFTLOB_X_SIDE
     if (((h & H_KIND) == H_ASK) & (sd != -1)) h |= H_RARE;  // (a common bid has side 1, a common ask -1)
+#ifdef HFTLOB_X_NN
+    if ((h <= H_BID) & (x.w < 0)) h |= H_RARE;  // a negative price (the common adds' note_add assumes p >= 0)
 #endif
     x.x = h;
     x.y = sd;
 }
-// returns false where the best quotes are known fresh afterwards (run_chunk's refresh test)
-// (HFTLOB_X_SIDE: d1 is the chunk's side register, read at lane k only where a handler needs it)
+// sdv: the chunk's side register (decode_msgs), read at lane k only where a handler needs the
+// side: a common (not RARE) bid has side 1 and a common ask -1, and only matches record it
 template <bool G, bool RC, int S>
-DEV bool process_msg_(Book<S>& B, u32 k, i32 h, i32 d1, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
+DEV void process_msg_(Book<S>& B, u32 k, i32 h, i32 sdv, i32 d2, i32 d3, i32 d4, i32 d5, i32 d6, i32 d7) {
     Msg m;
-#ifdef HFTLOB_X_SIDE
     m.h = h; m.side = 0; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
-#define HFTLOB_SIDE_RD(v) (m.side = (v))
-    const i32 sdv = d1;
-#else
-    m.h = h; m.side = d1; m.price = d3; m.qty = d2; m.oid = d4; m.tid = d5; m.t = d6; m.tns = d7;
-#define HFTLOB_SIDE_RD(v) ((void)0)
-#endif
     m.k = k;
-#ifdef HFTLOB_X_DISP
-    if (!G) {
-        const i32 cls = h & (H_KIND | H_RARE);
-        if (cls == H_BID) { HFTLOB_SIDE_RD(1); return bid_lim<G, false>(B, m); }
-        if (cls == H_ASK) { HFTLOB_SIDE_RD(-1); return ask_lim<G, false>(B, m); }
-    }
-#endif
     const i32 kind = h & H_KIND;
-    if (kind == H_CNL_ASK) return cancel<G, true, RC>(B, B.a, m);
-    else if (kind == H_CNL_BID) return cancel<G, false, RC>(B, B.b, m);
+    if (kind == H_CNL_ASK) cancel<G, true, RC>(B, B.a, m);
+    else if (kind == H_CNL_BID) cancel<G, false, RC>(B, B.b, m);
     else if (kind == H_BID) {
-        if (!G && !(h & H_RARE)) { HFTLOB_SIDE_RD(1); return bid_lim<G, false>(B, m); }
-        HFTLOB_SIDE_RD(rdl(sdv, k));
-        return bid_lim<G, true>(B, m);
+        if (!G && !(h & H_RARE)) {
+            m.side = 1;
+            bid_lim<G, false>(B, m);
+        } else {
+            m.side = rdl(sdv, k);
+            bid_lim<G, true>(B, m);
+        }
     } else if (kind == H_ASK) {
-        if (!G && !(h & H_RARE)) { HFTLOB_SIDE_RD(-1); return ask_lim<G, false>(B, m); }
-        HFTLOB_SIDE_RD(rdl(sdv, k));
-        return ask_lim<G, true>(B, m);
+        if (!G && !(h & H_RARE)) {
+            m.side = -1;
+            ask_lim<G, false>(B, m);
+        } else {
+            m.side = rdl(sdv, k);
+            ask_lim<G, true>(B, m);
+        }
     }
-    return false;  // (doNothing)
 }
-#undef HFTLOB_SIDE_RD
 
 // forward fill of -1 prices across the lanes of a chunk (carry = last price before it)
 DEV i32 ffill(i32 v, i32 carry) {
@@ -1266,9 +1269,10 @@ DEV i32 ffill(i32 v, i32 carry) {
 }
 // REC: after message k (which records the recomputed quotes), not at a chunk's start
 template <bool REC = true, int S> DEV void refresh_best(Book<S>& B, u32 k = 0) {
-    if (B.fl & (F_STALE_A | F_STALE_B)) {
+    if (B.fl & (STALE_ANY ? STALE_ANY : F_STALE_A | F_STALE_B)) {
         if (B.fl & F_STALE_A) rescan<true, REC>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint, k);
         if (B.fl & F_STALE_B) rescan<false, REC>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint, k);
+        B.fl &= ~STALE_ANY;
     }
 }
 
@@ -1394,27 +1398,16 @@ DEV void run_chunk(Book<S>& B, const int4& x, const int4& y, int cnt, int base, 
         // message k's fields are read (v_readlane) at the end of the message before it, so their
         // latency overlaps the best-quote record and the loop test instead of stalling the dispatch
         u32 k = ff1(todo);
-        i32 h = rdl(x.x, k), d1 = rdl(x.y, k), d2 = rdl(x.z, k), d3 = rdl(x.w, k), d4 = rdl(y.x, k),
+        i32 h = rdl(x.x, k), d2 = rdl(x.z, k), d3 = rdl(x.w, k), d4 = rdl(y.x, k),
             d5 = rdl(y.y, k), d6 = rdl(y.z, k), d7 = rdl(y.w, k);
         do {
             asm volatile("s_bitset0_b64 %0, %1" : "+s"(todo) : "s"(k));
             if (RC) B.mi = base + (int)k;
-#ifdef HFTLOB_X_SIDE
-            const i32 sd1 = x.y;
-#else
-            const i32 sd1 = d1;
-#endif
-            bool chk;
-            if ((i32)B.fl >= 0) chk = process_msg_<false, RC>(B, k, h, sd1, d2, d3, d4, d5, d6, d7);  // (!F_SLOW)
-            else chk = process_msg_<true, RC>(B, k, h, sd1, d2, d3, d4, d5, d6, d7);
-#ifdef HFTLOB_X_NOREF
-            if (chk) refresh_best(B, k);
-#else
-            (void)chk;
+            if ((i32)B.fl >= 0) process_msg_<false, RC>(B, k, h, x.y, d2, d3, d4, d5, d6, d7);  // (!F_SLOW)
+            else process_msg_<true, RC>(B, k, h, x.y, d2, d3, d4, d5, d6, d7);
             refresh_best(B, k);
-#endif
             const u32 kn = ff1(todo);  // (-1 once todo is empty: v_readlane takes the lane's low 6 bits)
-            h = rdl(x.x, kn); d1 = rdl(x.y, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
+            h = rdl(x.x, kn); d2 = rdl(x.z, kn); d3 = rdl(x.w, kn);
             d4 = rdl(y.x, kn); d5 = rdl(y.y, kn); d6 = rdl(y.z, kn); d7 = rdl(y.w, kn);
             k = kn;
         } while (todo);
@@ -1470,7 +1463,7 @@ __global__ __launch_bounds__(64) void k_book_process(hftlob_lob_cfg cfg, int n_e
     i32* ga = asks + (size_t)e * R * 6;
     i32* gb = bids + (size_t)e * R * 6;
     i32* gt = trades + (size_t)e * B.c.nT * 8;
-    B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs) | F_STALE_A | F_STALE_B;
+    B.fl = load_side<true>(B.a, ga, R, B.vs) | load_side<false>(B.b, gb, R, B.vs) | F_STALE_A | F_STALE_B | STALE_ANY;
     B.fl |= slow_bit(B.fl);
     load_trades(B.tr, gt, B.vt);
     {  // the loaded log's free-row prefix (see Book::ntr)
@@ -2951,9 +2944,9 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
     if (resident) {  // the book flags as the previous step left them (the cached best quotes are not kept)
         relink_side(B.a, R, B.vs);
         relink_side(B.b, R, B.vs);
-        B.fl = fl_carry | F_STALE_A | F_STALE_B;
+        B.fl = fl_carry | F_STALE_A | F_STALE_B | STALE_ANY;
     } else {
-        B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs) | F_STALE_A | F_STALE_B;
+        B.fl = commit_side<true>(B.a, fa, R, B.vs) | commit_side<false>(B.b, fb, R, B.vs) | F_STALE_A | F_STALE_B | STALE_ANY;
         B.fl |= slow_bit(B.fl);
     }
     SUBSTAMP(t_load);
