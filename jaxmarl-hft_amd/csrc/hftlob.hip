@@ -395,6 +395,9 @@ struct Side {
     i32* t;              // LDS table [6][R]
     i32* scr;            // LDS scratch row (64 words)
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid unless F_STALE
+#ifdef HFTLOB_X_XP
+    i32 xp;              // asks: the best price a bid crosses against (an empty side: maxint), with best_p
+#endif
     i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
                          // every handler reads prices, only adds and row clears write them
     // top-of-book cache: the slot _get_top_*_order_idx returns for max / min price top_p, and its
@@ -425,8 +428,8 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 
 // Wave-uniform book flags, one SGPR bitfield (bools would each be a 64-bit
 // lane mask the compiler copies at every merge):
-//   STALE  the side's cached best quote must be recomputed (one s_and tests both sides
-//          after a message)
+//   STALE  the side's cached best quote must be recomputed; STALE_ANY is set with either
+//          side's bit (SideBits::MARK), so the test after each message is one bit test
 //   CLEAN  every row with q <= 0 is an all -1 row => _removeZeroNegQuant only
 //          ever has to look at the row just written
 //   NEG1   some row with p != -1 holds a -1 in another field (then "first row
@@ -440,16 +443,7 @@ template <int S> DEV void col_set(i32 (&c)[S], int e, i32 v) {
 // + s_and_b64 exec + s_cbranch_vccnz, on any other bit to s_bitcmp1 + s_cbranch_scc)
 enum : u32 { F_STALE_A = 2, F_STALE_B = 4, F_CLEAN_A = 8, F_CLEAN_B = 16, F_NEG1_A = 32, F_NEG1_B = 64,
              F_PM1_A = 256, F_PM1_B = 512, F_STALE_ANY = 0x40000000u, F_SLOW = 0x80000000u };
-#ifdef HFTLOB_X_ANY
 constexpr u32 STALE_ANY = F_STALE_ANY;  // set with either side's STALE bit: one bit test after each message
-#else
-constexpr u32 STALE_ANY = 0;
-#endif
-#ifdef HFTLOB_X_NN
-constexpr bool NNADD = true;
-#else
-constexpr bool NNADD = false;
-#endif
 template <bool ASKS> struct SideBits {
     static constexpr u32 STALE = ASKS ? F_STALE_A : F_STALE_B;
     static constexpr u32 MARK = STALE | STALE_ANY;  // (sets STALE)
@@ -579,11 +573,13 @@ template <int S> DEV void best_bid_pq(const i32 (&p)[S], const i32 (&q)[S], cons
 }
 // get_best_ask: min price with -1 -> maxint, maxint -> -1; volume at it — :932-941
 template <int S>
-DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i32 maxint, i32& bp, i32& bq) {
+DEV void best_ask_pq(const i32 (&p)[S], const i32 (&q)[S], const Valid<S>& V, i32 maxint, i32& bp, i32& bq,
+                     i32* xp = nullptr) {
     i32 m = INT_MAX;
 #pragma unroll
     for (int r = 0; r < S; ++r) m = imin_(m, V.v[r] ? (p[r] == -1 ? maxint : p[r]) : INT_MAX);
     const i32 mn = wave_min(m);
+    if (xp) *xp = mn;  // (== pa, or maxint for an empty side or a maxint-only one: pa -1)
     const i32 pa = mn == maxint ? -1 : mn;
     i32 v = 0;
 #pragma unroll
@@ -597,7 +593,11 @@ template <bool ASKS, bool REC, int S>
 DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint, u32 k) {
     i32 q[S];
     ldcol(s.t, R, FQ, q);
+#ifdef HFTLOB_X_XP
+    if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q, &s.xp);
+#else
     if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q);
+#endif
     else best_bid_pq(s.pc, q, V, s.best_p, s.best_q);
     fl &= ~SideBits<ASKS>::STALE;
     if (REC) side_rec(s, k);
@@ -748,6 +748,11 @@ template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) 
 // STALE_OK = false: the caller knows the side is not stale (add_free: no message starts with a
 // stale side, run_chunk refreshes both after each one, and an add without eviction changes only
 // the other side before it gets here)
+#ifdef HFTLOB_X_XP
+#define XP_SET(s, v) ((s).xp = (v))
+#else
+#define XP_SET(s, v) ((void)0)
+#endif
 // NN: np >= 0 is known (the common adds: decode_msgs marks negative prices RARE)
 template <bool BID, int S, bool STALE_OK = true, bool NN = false>
 DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint, u32 k) {
@@ -775,10 +780,10 @@ DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i3
         if (np > bp) {
             if (bp == -1) {                 // empty side
                 if (np == maxint) fl |= MARK;
-                else { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
+                else { s.best_p = np; s.best_q = nq; XP_SET(s, np); side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
             }
         } else if (np < bp) {
-            if (NN || np != -1) { s.best_p = np; s.best_q = nq; side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
+            if (NN || np != -1) { s.best_p = np; s.best_q = nq; XP_SET(s, np); side_rec(s, k); top_new(s, e, np, t, tns, maxint); }
         } else if (!NN && np == -1) {
             fl |= MARK;
         } else if (np != maxint) {
@@ -933,7 +938,7 @@ DEV i32 match_against(Book<S>& B, Side<S>& s, i32 qtm, i32 price, const Msg& m) 
 template <bool BID, bool G, int S>
 DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
-    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, STALE = SideBits<!BID>::MARK,
+    constexpr u32 CLEAN = SideBits<!BID>::CLEAN, NEG1 = SideBits<!BID>::NEG1, MARK = SideBits<!BID>::MARK,
                   PM1 = SideBits<!BID>::PM1;
     const i32 nq = imax_(0, qty);
     if (!G) {  // FAST: "any -1" <=> p == -1 <=> an all -1 row; no free slot -> the last slot, which holds an order
@@ -943,10 +948,10 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
             side_put(s, R, e, m.price, nq, m.oid, m.tid, m.t, m.tns);
             if (m.h & (H_NEG1 | H_PM1)) B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
             if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint, m.k);
-            else { B.fl |= STALE; s.top = -1; }
+            else { B.fl |= MARK; s.top = -1; }
         } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
             side_clr(s, R, e);
-            B.fl |= STALE;
+            B.fl |= MARK;
         }
         return;
     }
@@ -979,10 +984,10 @@ DEV void add_order(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&
         if (m.h & H_NEG1) B.fl |= NEG1;
         if (m.h & H_PM1) B.fl |= PM1;
         if (was_empty) note_add<BID>(s, B.fl, e, m.price, nq, m.t, m.tns, B.c.maxint, m.k);
-        else { B.fl |= STALE; s.top = -1; }
+        else { B.fl |= MARK; s.top = -1; }
     } else if (!was_empty) {  // the new row is removed at once: net effect clears row e
         side_clr(s, R, e);
-        B.fl |= STALE;
+        B.fl |= MARK;
     }
 }
 
@@ -1028,7 +1033,7 @@ DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&f
         constexpr u32 NEG1 = SideBits<!BID>::NEG1, PM1 = SideBits<!BID>::PM1;
         B.fl = B.fl | (m.h & H_NEG1 ? NEG1 : 0u) | (m.h & H_PM1 ? PM1 : 0u) | F_SLOW;
     }
-    note_add<BID, S, false, NNADD && !RARE>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint, m.k);
+    note_add<BID, S, false, !RARE>(s, B.fl, (int)e, m.price, qty, m.t, m.tns, B.c.maxint, m.k);
 }
 // bid_lim — :357-420 (the eviction persists when the add is discarded)
 // RARE = false: the message has none of the H_RARE flags (MKT, discard, -1 fields), so their
@@ -1037,8 +1042,12 @@ template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     constexpr bool POS = !RARE && !G;
     if (POS) {  // the common add: it does not cross (an empty ask side stands for maxint), so all of it goes in
+#ifdef HFTLOB_X_XP
+        if (__builtin_expect(B.a.xp > m.price, 1)) {
+#else
         const i32 bp = B.a.best_p;
         if (__builtin_expect((bp == -1 ? B.c.maxint : bp) > m.price, 1)) {
+#endif
             lmask free[S];
             free_slots(B, B.b, free);
             if (!no_slot(free)) {
@@ -1224,9 +1233,7 @@ DEV void decode_msgs(const LobCfg& c, int4& x, const int4& y) {
     if (h & (H_DISCARD | H_NEG1 | H_PM1 | H_MKT)) h |= H_RARE;
     if ((h <= H_BID) & (x.z <= 0)) h |= H_RARE;  // an add of no quantity (the common add handlers assume qty > 0)
     if (((h & H_KIND) == H_ASK) & (sd != -1)) h |= H_RARE;  // (a common bid has side 1, a common ask -1)
-#ifdef HFTLOB_X_NN
     if ((h <= H_BID) & (x.w < 0)) h |= H_RARE;  // a negative price (the common adds' note_add assumes p >= 0)
-#endif
     x.x = h;
     x.y = sd;
 }
@@ -1269,7 +1276,7 @@ DEV i32 ffill(i32 v, i32 carry) {
 }
 // REC: after message k (which records the recomputed quotes), not at a chunk's start
 template <bool REC = true, int S> DEV void refresh_best(Book<S>& B, u32 k = 0) {
-    if (B.fl & (STALE_ANY ? STALE_ANY : F_STALE_A | F_STALE_B)) {
+    if (B.fl & STALE_ANY) {
         if (B.fl & F_STALE_A) rescan<true, REC>(B.a, B.fl, B.c.nO, B.vs, B.c.maxint, k);
         if (B.fl & F_STALE_B) rescan<false, REC>(B.b, B.fl, B.c.nO, B.vs, B.c.maxint, k);
         B.fl &= ~STALE_ANY;
