@@ -395,9 +395,7 @@ struct Side {
     i32* t;              // LDS table [6][R]
     i32* scr;            // LDS scratch row (64 words)
     i32 best_p, best_q;  // get_best_{ask,bid} price and get_volume_at_price(best); valid unless F_STALE
-#ifdef HFTLOB_X_XP
     i32 xp;              // asks: the best price a bid crosses against (an empty side: maxint), with best_p
-#endif
     i32 pc[S];           // the price column, lane-strided in VGPRs (a write-through copy of field FP):
                          // every handler reads prices, only adds and row clears write them
     // top-of-book cache: the slot _get_top_*_order_idx returns for max / min price top_p, and its
@@ -593,11 +591,7 @@ template <bool ASKS, bool REC, int S>
 DEV void rescan(Side<S>& s, u32& fl, int R, const Valid<S>& V, i32 maxint, u32 k) {
     i32 q[S];
     ldcol(s.t, R, FQ, q);
-#ifdef HFTLOB_X_XP
     if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q, &s.xp);
-#else
-    if (ASKS) best_ask_pq(s.pc, q, V, maxint, s.best_p, s.best_q);
-#endif
     else best_bid_pq(s.pc, q, V, s.best_p, s.best_q);
     fl &= ~SideBits<ASKS>::STALE;
     if (REC) side_rec(s, k);
@@ -748,11 +742,7 @@ template <int S> DEV void top_eq(Side<S>& s, int e, i32 t, i32 tns, i32 maxint) 
 // STALE_OK = false: the caller knows the side is not stale (add_free: no message starts with a
 // stale side, run_chunk refreshes both after each one, and an add without eviction changes only
 // the other side before it gets here)
-#ifdef HFTLOB_X_XP
-#define XP_SET(s, v) ((s).xp = (v))
-#else
-#define XP_SET(s, v) ((void)0)
-#endif
+#define XP_SET(s, v) ((s).xp = (v))  // (asks: a new best price below maxint)
 // NN: np >= 0 is known (the common adds: decode_msgs marks negative prices RARE)
 template <bool BID, int S, bool STALE_OK = true, bool NN = false>
 DEV void note_add(Side<S>& s, u32& fl, int e, i32 np, i32 nq, i32 t, i32 tns, i32 maxint, u32 k) {
@@ -1042,12 +1032,7 @@ template <bool G, bool RARE, int S> DEV void bid_lim(Book<S>& B, Msg m) {
     if (!RARE) __builtin_assume(m.qty > 0);  // (decode_msgs: an add of no quantity is RARE)
     constexpr bool POS = !RARE && !G;
     if (POS) {  // the common add: it does not cross (an empty ask side stands for maxint), so all of it goes in
-#ifdef HFTLOB_X_XP
-        if (__builtin_expect(B.a.xp > m.price, 1)) {
-#else
-        const i32 bp = B.a.best_p;
-        if (__builtin_expect((bp == -1 ? B.c.maxint : bp) > m.price, 1)) {
-#endif
+        if (__builtin_expect(B.a.xp > m.price, 1)) {  // (xp: the best ask, an empty side maxint)
             lmask free[S];
             free_slots(B, B.b, free);
             if (!no_slot(free)) {
@@ -3176,8 +3161,10 @@ DEV bool env_step_dev(const hftlob_env_cfg& c, int key_n, int ek, int e, const u
         if (row < M) {
             const float mf = i2f(wadd(cbp, cap)) / 2.0f;
             mid_acc = base == 0 ? mf : mid_acc + mf;
-            pa_acc = base == 0 ? i2f(cap) : pa_acc + i2f(cap);
-            pb_acc = base == 0 ? i2f(cbp) : pb_acc + i2f(cbp);
+            if (info_out) {  // (the info's average quotes only)
+                pa_acc = base == 0 ? i2f(cap) : pa_acc + i2f(cap);
+                pb_acc = base == 0 ? i2f(cbp) : pb_acc + i2f(cbp);
+            }
         }
         if (base + 64 >= M) {  // final time = last combined row's (s, ns)
             last_t0 = rdl(y.z, cnt - 1);
