@@ -194,3 +194,23 @@ def noop_streams(n_env, n_msg, seed, price0=1000, nO=100):
                 price = price0 + side * 4
             out[e, k] = (typ, side, qty, price, oid, tid, t, tn)
     return out
+
+
+def odd_add_streams(n_env, n_msg, seed, price0=1000, maxint=2**31 - 1):
+    """random_streams whose adds include the kernel's RARE decode cases (hftlob.hip decode_msgs):
+    limit and type-4 messages priced at or below 0 (-1, -2, -7: a negative ask crosses every bid,
+    a negative bid rests behind them all), priced maxint, and add-kind messages whose side is not
+    -1 / 1 (type 1 with side 0 or 2 is an ask_lim with that side, as cond_type_side sends it;
+    type 4 with side 0 / 2 flips to 0 / -2).  The common add handlers assume 0 <= price, qty > 0
+    and side -1 / 1; these must take the general path and leave the book exactly as the oracle's."""
+    out = random_streams(n_env, n_msg, seed, price0=price0)
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    add = (out[..., 0] == 1) | (out[..., 0] == 4)
+    u = rng.random(out.shape[:2])
+    neg = add & (u < 0.06)
+    out[..., 3] = np.where(neg, rng.choice([-1, -2, -7, 0], size=out.shape[:2]), out[..., 3])
+    top = add & (u >= 0.06) & (u < 0.08)
+    out[..., 3] = np.where(top, maxint, out[..., 3])
+    odd = add & (u >= 0.08) & (u < 0.13)
+    out[..., 1] = np.where(odd, rng.choice([0, 2, -2], size=out.shape[:2]), out[..., 1])
+    return out

@@ -9,7 +9,8 @@ from hftlob.config import JAXLOB_Configuration
 from hftlob.engine import book_process_, scan_through_entire_array_save_bidask
 from hftlob.layout import pack_lob_cfg
 from oracle import pyoracle as O
-from streams import full_book_messages, init_book_messages, neg1_trade_streams, noop_streams, random_streams, top_streams
+from streams import (full_book_messages, init_book_messages, neg1_trade_streams, noop_streams, odd_add_streams,
+                     random_streams, top_streams)
 
 pytestmark = pytest.mark.gpu
 
@@ -92,6 +93,23 @@ def test_book_empty_and_max_sizes():
     empty_t = np.full((E, 256, 8), -1, np.int32)
     a0, b0, _, _, _ = O.book_process(pack_lob_cfg(big), init, empty_a, empty_a, empty_t, save_best=False)
     _run(big, random_streams(E, M, seed=77), a0, b0, empty_t)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(nOrders=16, nTrades=8), dict(type_4_interpretation=1),
+                                dict(type_4_interpretation=2)], ids=["default", "nO16", "t4lim", "t4mkt"])
+def test_book_odd_adds(kw):
+    """Adds priced <= 0 or maxint and add-kind messages whose side is not -1 / 1
+    (streams.odd_add_streams): the decode marks them RARE, the general handlers take them, and
+    the common handlers that follow see the book they left (negative-price rows, full sides)."""
+    cfg = JAXLOB_Configuration(**kw)
+    E, M = 64, 400
+    init = init_book_messages(E, seed=6)
+    empty_a = np.full((E, cfg.nOrders, 6), -1, np.int32)
+    empty_t = np.full((E, cfg.nTrades, 8), -1, np.int32)
+    a0, b0, _, _, _ = O.book_process(pack_lob_cfg(cfg), init, empty_a, empty_a, empty_t, save_best=False)
+    msgs = odd_add_streams(E, M, seed=31 + cfg.nOrders)
+    _run(cfg, msgs, a0, b0, empty_t)
+    _run(cfg, msgs, empty_a, empty_a, empty_t)
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(nOrders=16, nTrades=8), dict(type_4_interpretation=1)],
