@@ -141,8 +141,8 @@ def noop_streams(n_env, n_msg, seed, price0=1000, nO=100):
     cancel: its -1 index wraps to the last slot), at prices that do and do not hold init-id rows,
     with quantities 1..50, 0, -1 (skippable) and below -1 (which end the skipping); doNothing rows;
     cancels of live ids and of id -1; non-crossing adds that fill the last free rows of a side
-    (the room test's boundary), adds carrying an init id or a -1 field (which end the skipping),
-    and executions."""
+    (the room test's boundary), adds of no quantity (into sides with and without a free row),
+    adds carrying an init id or a -1 field (which end the skipping), and executions."""
     rng = np.random.Generator(np.random.PCG64(seed))
     out = np.zeros((n_env, n_msg, 8), dtype=np.int32)
     for e in range(n_env):
@@ -157,10 +157,13 @@ def noop_streams(n_env, n_msg, seed, price0=1000, nO=100):
             qty = int(rng.integers(1, 50))
             tid = int(rng.integers(1, 6))
             u = rng.random()
-            if u < 0.25:                      # non-crossing add
+            if u < 0.25:                      # non-crossing add (a fifth of no quantity: a full side evicts for them)
                 typ, oid = 1, next_oid
                 next_oid += 1
-                live.append((oid, side, price))
+                if rng.random() < 0.2:
+                    qty = int(rng.choice([0, 0, -1, -4]))
+                else:
+                    live.append((oid, side, price))
             elif u < 0.62:                    # cancel of an id no row holds
                 typ = int(rng.choice([2, 3]))
                 oid = int(rng.integers(1, 10**6))
@@ -188,10 +191,12 @@ def noop_streams(n_env, n_msg, seed, price0=1000, nO=100):
             elif u < 0.95:                    # execution
                 typ = 4
                 oid = live[int(rng.integers(0, len(live)))][0] if live else 7
-            else:                             # marketable limit
+            else:                             # marketable limit (sometimes of no quantity: it matches nothing)
                 typ, oid = 1, next_oid
                 next_oid += 1
                 price = price0 + side * 4
+                if rng.random() < 0.2:
+                    qty = 0
             out[e, k] = (typ, side, qty, price, oid, tid, t, tn)
     return out
 
