@@ -1013,10 +1013,23 @@ template <bool BID, bool RARE, int S, bool POS = false>
 DEV void add_free(Book<S>& B, Side<S>& s, const Msg& m, i32 qty, const lmask (&free)[S]) {
     const int R = B.c.nO;
     if (!POS && qty <= 0) return;  // imax(0, qty) == 0: the new row is removed at once and the slot was empty
-    u32 e = ff1(free[0]);
+    u32 e;
+    if (S == 2) {  // the slot's register set is known from the branch: one v_writelane updates the price column
+        if (free[0] != 0ull) {
+            e = ff1(free[0]);
+            s.pc[0] = wlane(s.pc[0], m.price, (int)e);
+        } else {
+            e = ff1(free[S - 1]);
+            s.pc[S - 1] = wlane(s.pc[S - 1], m.price, (int)e);
+            e |= 64u;
+        }
+        st6(s.t, s.scr, R, (int)e, m.price, qty, m.oid, m.tid, m.t, m.tns);
+    } else {
+        e = ff1(free[0]);
 #pragma unroll
-    for (int r = 1; r < S; ++r) e = min(e, ff1(free[r]) | (u32)(64 * r));
-    side_put(s, R, (int)e, m.price, qty, m.oid, m.tid, m.t, m.tns);
+        for (int r = 1; r < S; ++r) e = min(e, ff1(free[r]) | (u32)(64 * r));
+        side_put(s, R, (int)e, m.price, qty, m.oid, m.tid, m.t, m.tns);
+    }
     if (RARE && __builtin_expect((m.h & (H_NEG1 | H_PM1)) != 0, 0)) {
         // rare: kept as a branch (the empty asm stops if-conversion into ~10 scalar selects per add)
         asm volatile("");
